@@ -1,0 +1,315 @@
+#!/usr/bin/env python3
+"""Benchmark: Q4_0 x Q8_1 W4A8 GEMV on MI355X (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload:
+  * N=1: BASELINE configs[1] — M=1, N=4096, K=4096, Q4_0 weights x Q8_1 activations.
+  * N>1: row-sharded GEMV, 4000 weight rows per GPU (N=8 -> BASELINE configs[4], N=32000), each
+    step's output slices all-gathered over RCCL (xGMI) on torch's NCCL stream, overlapped with the
+    next step's kernels. Per-GPU work is fixed -> "scaling": "weak".
+  * One step = G (default 64) independent GEMVs, each on a DIFFERENT resident weight copy (64 x
+    9.4 MB = 604 MB > the 256 MB Infinity Cache), so every launch streams its weights from HBM
+    (the decode situation: a model's layers are read once per token). Activations are one
+    replicated Q8_1 vector already in HBM. The step's G launches are captured in a hipGraph.
+  * value = effective TFLOPS (2*M*N*K per GEMV, all ranks) over the timed steps; "gbps" is the
+    matching algorithmic byte rate (tests/benchmark/benchmark_comparison.cu:138-140 formula).
+  * roofline.achieved = algorithmic bytes of ONE launch / that kernel's average duration, measured
+    live with HIP events bracketing each launch on the launch stream (a separate eager pass over
+    the same rotation, so the event records do not perturb the timed graph replays).
+  * cpu_baseline (rank 0, N=1): the oracle's restatement of gemm_w4a8_reference
+    (include/gemm_reference.h:175-222) on the step4 input recipe, 1 thread, ~10 s sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "llama.cpp-quant-gemm_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import quant_gemm as qg  # noqa: E402
+from quant_gemm.sharded import rows_per_rank, shard_rows  # noqa: E402
+
+METRIC = "effective TFLOPS + GB/s, Q4_0×Q8_1 GEMV M=1 N=K=4096; NMSE vs FP32"
+REF_GFLOPS = 622.3  # best published Q4_0xQ8_1 GEMV, M=1 N=K=4096 (RTX 5070 Laptop)
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+WTYPES = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
+
+
+def algo_bytes(m: int, n: int, k: int, bb: int) -> int:
+    """N*(K/32)*S_w + M*(K/32)*36 + M*N*4 (tests/benchmark/benchmark_comparison.cu:138-140)."""
+    nb = k // 32
+    return n * nb * bb + m * nb * 36 + m * n * 4
+
+
+def load_traffic(cfg_key: str):
+    """HBM bytes per launch from the committed PMC profile (profiles/*pmc*.json), if present."""
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir), reverse=True):
+        if f.endswith(".json") and "pmc" in f:
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except (OSError, ValueError):
+                continue
+            v = d.get(cfg_key, {}).get("hbm_bytes_per_launch")
+            if v:
+                return float(v)
+    return None
+
+
+def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O  # the checker / CPU baseline only
+    a, b = O.fill_uniform_step4(m, n, k, 42)
+    aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, wtype)
+    O.gemm_w4a8(aq, bq, wtype)  # warm-up
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        O.gemm_w4a8(aq, bq, wtype)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    per = el / runs
+    threads = min(16, os.cpu_count() or 1)
+    t1 = time.perf_counter()
+    mt_runs = 0
+    while time.perf_counter() - t1 < max(1.0, seconds / 5):
+        O.gemm_w4a8_mt(aq, bq, wtype, threads)
+        mt_runs += 1
+    per_mt = (time.perf_counter() - t1) / mt_runs
+    flops = 2.0 * m * n * k
+    return ({"value": flops / per / 1e12, "unit": "TFLOPS", "cores": 1, "kind": "port",
+             "ms_per_gemv": per * 1e3,
+             "sample": f"oracle/qg_oracle.c gemm_w4a8 (restates include/gemm_reference.h:175-222), "
+                       f"M={m} N={n} K={k}, {runs} runs in {el:.1f} s, 1 thread, step4 srand(42) inputs"},
+            {"value": flops / per_mt / 1e12, "unit": "TFLOPS", "cores": threads, "ms_per_gemv": per_mt * 1e3,
+             "sample": f"row-partitioned over {threads} threads, {mt_runs} runs"})
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--gemvs-per-step", type=int, default=64)
+    ap.add_argument("--wtype", default="q4_0", choices=sorted(WTYPES))
+    ap.add_argument("--m", type=int, default=1)
+    ap.add_argument("--n", type=int, default=0, help="total weight rows (default 4096 at 1 GPU, 4000/GPU beyond)")
+    ap.add_argument("--k", type=int, default=4096)
+    ap.add_argument("--algo", type=int, default=0)
+    ap.add_argument("--copy-bytes", type=float, default=600e6, help="resident weight bytes to rotate through")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    wtype = WTYPES[args.wtype]
+    bb = qg.BLOCK_BYTES[wtype]
+    M, K, G = args.m, args.k, args.gemvs_per_step
+    n_total = args.n or (4096 if world == 1 else 4000 * world)
+    rows = rows_per_rank(n_total, world)
+    s0, s1 = shard_rows(n_total, world, rank)
+    local = s1 - s0
+
+    # ---- synthetic data, generated and quantized on the GPU by the product's own kernels
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42)
+    a = torch.rand((M, K), generator=gen, device=dev) * 2 - 1          # replicated activations
+    gen.manual_seed(1000 + rank)
+    b = torch.rand((local, K), generator=gen, device=dev) * 2 - 1      # this rank's weight rows
+    aq = qg.quantize_q8_1(a)
+    bq = qg.quantize(b, wtype)
+    shard_bytes = bq.numel()
+    R = max(G, math.ceil(args.copy_bytes / max(shard_bytes, 1)))
+    wcopies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
+    wcopies.copy_(bq.unsqueeze(0).expand_as(wcopies))
+    outs = [torch.zeros((G, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((G, world, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+
+    # accuracy of this run's data: NMSE vs an fp64 matmul of the unquantized inputs
+    c = qg.gemm_w4a8(aq, bq, M, local, K, wtype)
+    ref = a.double() @ b.double().T
+    num = torch.sum((c.double() - ref) ** 2)
+    den = torch.sum(ref ** 2)
+    if world > 1:
+        nd = torch.stack([num, den])
+        dist.all_reduce(nd)
+        num, den = nd[0], nd[1]
+    nmse = float(num / den)
+    del b, ref, c
+
+    lib = qg._lib.load()
+    fn = lib.qg_gemm_w4a8_ex
+    a_ptr = ctypes.c_void_p(aq.data_ptr())
+    w_ptrs = [ctypes.c_void_p(wcopies[i].data_ptr()) for i in range(R)]
+    o_ptrs = [[ctypes.c_void_p(outs[s][j].data_ptr()) for j in range(G)] for s in range(2)]
+
+    def launch(j: int, s: int, copy: int, stream) -> None:
+        st = fn(a_ptr, w_ptrs[copy], o_ptrs[s][j], M, local, K, wtype, args.algo, stream)
+        if st != 0:
+            raise RuntimeError(f"qg_gemm_w4a8_ex failed: {st}")
+
+    def step_eager(s: int, base: int = 0) -> None:
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for j in range(G):
+            launch(j, s, (base + j) % R, stream)
+
+    # ---- hipGraph of one step per output buffer
+    graphs = None
+    if not args.no_graph:
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            step_eager(0)
+            step_eager(1)
+        torch.cuda.synchronize()
+        graphs = []
+        for s in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step_eager(s)
+            graphs.append(g)
+
+    pending = [None, None]
+
+    def run_step(i: int) -> None:
+        s = i % 2
+        if pending[s] is not None:
+            pending[s].wait()           # the gather that read outs[s] two steps ago
+            pending[s] = None
+        if graphs is not None:
+            graphs[s].replay()
+        else:
+            step_eager(s)
+        if world > 1:
+            pending[s] = dist.all_gather_into_tensor(gathered[s].view(-1), outs[s].view(-1), async_op=True)
+
+    def drain() -> None:
+        for s in range(2):
+            if pending[s] is not None:
+                pending[s].wait()
+                pending[s] = None
+
+    for i in range(args.warmup):
+        run_step(i)
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run_step(i)
+    drain()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-launch kernel duration: HIP events bracketing each launch on its stream
+    n_ev = 4 * G
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    cur = torch.cuda.current_stream()
+    stream = ctypes.c_void_p(cur.cuda_stream)
+    for i in range(n_ev):
+        evs[i][0].record(cur)
+        launch(i % G, 0, i % R, stream)
+        evs[i][1].record(cur)
+    torch.cuda.synchronize()
+    durs = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in evs)  # us
+    kern_us = sum(durs) / len(durs)
+    kern_med = durs[len(durs) // 2]
+
+    # ---- hot (Infinity-Cache resident) reference point: one copy, same launch count
+    hot_us = None
+    if graphs is not None:
+        g_hot = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_hot):
+            stream_c = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for j in range(G):
+                launch(j, 0, 0, stream_c)
+        for _ in range(3):
+            g_hot.replay()
+        torch.cuda.synchronize()
+        th = time.perf_counter()
+        for _ in range(10):
+            g_hot.replay()
+        torch.cuda.synchronize()
+        hot_us = (time.perf_counter() - th) / (10 * G) * 1e6
+
+    flops_per_gemv = 2.0 * M * n_total * K
+    total_flops = flops_per_gemv * G * args.steps
+    bytes_per_gemv_all = n_total * (K // 32) * bb + world * M * (K // 32) * 36 + M * n_total * 4
+    launch_bytes = algo_bytes(M, local, K, bb)
+    value = total_flops / elapsed / 1e12
+    achieved = launch_bytes / (kern_us * 1e-6) / 1e9
+    cfg_key = f"{args.wtype}_m{M}_n{local}_k{K}"
+    traffic = load_traffic(cfg_key)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "TFLOPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value * 1e3 / REF_GFLOPS, 3),
+            "dtype": "int8",
+            "data": "synthetic U[-1,1) (torch Generator), quantized on-GPU to Q8_1/Q4_0 by the product's quantizers",
+            "config": {"workload": f"{args.wtype}_q8_1_gemv", "M": M, "N": n_total, "K": K,
+                       "rows_per_gpu": local, "gemvs_per_step": G, "weight_copies": R,
+                       "parallelism": f"row-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                       "launch": "hipGraph" if graphs is not None else "eager",
+                       "kernel_algo": int(qg.select_algo(M, local, K, wtype)) if args.algo == 0 else args.algo},
+            "gbps": round(bytes_per_gemv_all * G * args.steps / elapsed / 1e9, 1),
+            "us_per_gemv": round(elapsed / (args.steps * G) * 1e6, 3),
+            "nmse_vs_fp32": nmse,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel_us_mean": round(kern_us, 3), "kernel_us_median": round(kern_med, 3),
+                         "bytes_per_launch": launch_bytes},
+            "hot_l3": None if hot_us is None else {"us_per_gemv": round(hot_us, 3),
+                                                   "tflops": round(flops_per_gemv / world / hot_us / 1e6, 3)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            one, mt = cpu_baseline(M, n_total, K, wtype, args.cpu_seconds)
+            out["cpu_baseline"] = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in one.items()}
+            out["cpu_baseline_mt"] = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in mt.items()}
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

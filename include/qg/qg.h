@@ -1,0 +1,120 @@
+/*
+ * qg/qg.h — C-ABI of the MI355X (gfx950) W4A8 quantized GEMM/GEMV library `libqg_hip.so`.
+ *
+ * Plain C: raw device pointers, sizes, an opaque HIP stream. Every call is stream-ordered and
+ * asynchronous (no host sync), stateless and reentrant; the caller owns all buffers
+ * (destination-passing, schemas/docs/solution.md:27-42). Unlike the reference's `void` launch
+ * wrappers (include/gemm_cuda_naive.cuh:285-292 — no error check), every entry point returns a
+ * qg_status: 0 on success, a negative code otherwise; nothing is launched on a validation error.
+ *
+ * Conventions (the two-convention trap):
+ *   activation-major  C[M][N] = A_q8_1[M][K] . B_w[N][K]^T   M = tokens, N = weight rows
+ *                     (include/gemm_reference.h:7-13, 175-222; include/llama_adapter.h)
+ *   weight-major      out[M][N] = W[M][K] . A_q8_1[N][K]^T   M = weight rows, N = tokens
+ *                     (kernels/gemm/gemm_quant_formats.cuh:312-334, python/quant_gemm)
+ * Block layouts: qg/blocks.h (byte-identical to include/quant_types.h / compat/ggml_types.h).
+ */
+#ifndef QG_QG_H
+#define QG_QG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Binary-compatible with hipStream_t (NULL = the default stream). */
+typedef struct ihipStream_t* qg_stream_t;
+
+/* Quantization type ids = ggml_type ids (compat/ggml_types.h:199-215). */
+typedef enum {
+    QG_TYPE_F32 = 0,
+    QG_TYPE_F16 = 1,
+    QG_TYPE_Q4_0 = 2,
+    QG_TYPE_Q4_1 = 3,
+    QG_TYPE_Q5_0 = 6,
+    QG_TYPE_Q5_1 = 7,
+    QG_TYPE_Q8_0 = 8,
+    QG_TYPE_Q8_1 = 9
+} qg_type;
+
+typedef enum {
+    QG_OK = 0,
+    QG_ERR_INVALID_ARG = -1, /* null pointer, negative size, unknown kernel_type */
+    QG_ERR_BAD_K = -2,       /* K (or element count) not a positive multiple of 32 */
+    QG_ERR_UNSUPPORTED = -3, /* weight type / algorithm not available for this shape */
+    QG_ERR_ALIGN = -4,       /* pointer alignment below what the block format allows */
+    QG_ERR_HIP = -5          /* HIP launch error (see qg_last_hip_error) */
+} qg_status;
+
+/* Kernel family selection for qg_gemm_w4a8_ex (QG_ALGO_AUTO picks by shape). */
+typedef enum {
+    QG_ALGO_AUTO = 0,
+    QG_ALGO_GEMV = 1,    /* M <= 8: register-resident super-block decode + v_dot4 */
+    QG_ALGO_MFMA = 2,    /* M > 8: LDS-staged activations, v_mfma_i32_32x32x32_i8 per Q-block */
+    QG_ALGO_GENERIC = 3  /* any K % 32 == 0, any alignment */
+} qg_algo;
+
+/* ---- W4A8 GEMM, activation-major ---------------------------------------------------------
+ * Replaces gemm_w4a8_{naive,tiled,dp4a,tiled_dp4a,vectorized_dp4a}(A, B, C, M, N, K, stream)
+ * (include/gemm_cuda_naive.cuh:285-292, gemm_cuda_tiled.cuh:293-300, gemm_cuda_dp4a.cuh:409-444)
+ * and is the device twin of gemm_w4a8_reference (include/gemm_reference.h:175-222).
+ * A: block_q8_1[M][K/32]; B: blocks of `wtype` (Q4_0/Q4_1/Q5_0/Q5_1) [N][K/32]; C: float[M][N],
+ * overwritten. M == 0 or N == 0 is a no-op. */
+int qg_gemm_w4a8(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, qg_stream_t stream);
+int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, int algo,
+                    qg_stream_t stream);
+
+/* ---- weight-major twins (kernels/gemm/gemm_quant_formats.cuh:343-428) ---------------------
+ * out[M][N] = W[M][K/32] . A[N][K/32]^T, M = weight rows, N = tokens. */
+int qg_gemm_q4_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_q4_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_q5_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_q5_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+
+/* ---- quantizers (include/quantize.h:343-368; python/quant_gemm/csrc/gemm_ops.cu:146-202) ----
+ * x: float[k] (k = total elements, multiple of 32), y: k/32 blocks of the named type.
+ * Bytes are identical to the reference CPU quantizers (quantize_row_*_ref, round half away). */
+int qg_quantize_q8_1(const float* x, void* y, int64_t k, qg_stream_t stream);
+int qg_quantize_q4_0(const float* x, void* y, int64_t k, qg_stream_t stream);
+/* Any type; variant 0 = include/quantize.h semantics, variant 1 (Q8_1 only) =
+ * tests/framework/test_framework.cuh:195-225 (s = d * sum(q), q clamped to +-127). Q4_1/Q5_0/Q5_1
+ * follow tests/framework/test_framework.cuh:256-367. */
+int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_stream_t stream);
+/* Dequantize k elements (include/quantize.h:84-102 and the per-format formulas). */
+int qg_dequantize(int type, const void* x, float* y, int64_t k, qg_stream_t stream);
+int qg_dequantize_q4_0(const void* x, float* y, int64_t k, qg_stream_t stream);
+
+/* ---- parity hook: per-block int32 dots sumi[M][N][K/32] through the SAME decode path the
+ * chosen algorithm uses (the reference's inner loop, include/gemm_reference.h:202-212). */
+int qg_debug_sumi(const void* A_q8_1, const void* B, int32_t* sumi, int M, int N, int K, int wtype, int algo,
+                  qg_stream_t stream);
+
+/* ---- ggml-facing adapter (include/llama_adapter.h:49-76, declared but never defined there) ----
+ * A minimal ggml_tensor view: ne[0] = K (contiguous), ne[1] = rows; nb[] byte strides.
+ * activation: Q8_1 [K, M]; weights: Q4_0/Q4_1/Q5_0/Q5_1 [K, N]; output: F32 [N, M] (ggml
+ * ne-order), i.e. row-major C[M][N]. kernel_type: NULL or any of the reference's names
+ * ("naive", "tiled", "dp4a", "tiled_dp4a", "vectorized_dp4a") or "auto"/"gemv"/"mfma"/"generic". */
+typedef struct {
+    void* data;
+    int type;       /* qg_type */
+    int64_t ne[4];  /* elements per dim, ne[0] innermost */
+    size_t nb[4];   /* byte stride per dim */
+} qg_tensor_view;
+
+int qg_gemm_w4a8_from_view(const qg_tensor_view* activation, const qg_tensor_view* weights, qg_tensor_view* output,
+                           const char* kernel_type, qg_stream_t stream);
+
+/* ---- introspection ---- */
+const char* qg_status_string(int status);
+int qg_last_hip_error(void);                    /* hipError_t of the last QG_ERR_HIP on this thread */
+int qg_select_algo(int M, int N, int K, int wtype); /* what QG_ALGO_AUTO dispatches to */
+int qg_block_bytes(int type);                   /* 18/20/22/24/34/36, 0 if unknown */
+const char* qg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QG_QG_H */

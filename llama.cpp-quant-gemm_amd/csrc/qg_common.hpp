@@ -1,0 +1,120 @@
+// qg_common.hpp — device-side building blocks shared by every W4A8 kernel (gfx950 only).
+//
+// Block formats are the byte-exact llama.cpp ones (include/qg/blocks.h). Everything here works on
+// raw dwords already in VGPRs: a block's fields are pulled out of a register-resident "super-block"
+// (8 consecutive blocks = 256 elements, 144/160/176/192 B for Q4_0/Q4_1/Q5_0/Q5_1 — always a
+// multiple of 16 B, so a lane can fetch it with global_load_dwordx4) with compile-time byte offsets,
+// i.e. v_alignbyte_b32 / shifts, never LDS or byte loads.
+//
+// Per-block epilogues restate the reference formulas operation for operation (no contraction; the
+// library is built with -ffp-contract=off) so a block's fp32 term is bit-identical to the CPU
+// oracle's:
+//   Q4_0  d_w * (d_a * sumi - 8 * s_a)        include/gemm_reference.h:216
+//   Q5_0  d_w * (d_a * sumi - 16 * s_a)       kernels/gemm/gemm_quant_formats.cuh:207
+//   Q4_1  d_w * d_a * sumi + m_w * s_a        flashinfer_trace/definitions/quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json:79
+//   Q5_1  d_w * d_a * sumi + m_w * s_a        (the reference's /4 at gemm_quant_formats.cuh:148,266 is a
+//                                              mis-port and is NOT reproduced; SURVEY.md §0 defect 2)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include <utility>
+
+namespace qg {
+
+// ggml_type ids (compat/ggml_types.h:199-215)
+enum : int { FMT_Q4_0 = 2, FMT_Q4_1 = 3, FMT_Q5_0 = 6, FMT_Q5_1 = 7, FMT_Q8_0 = 8, FMT_Q8_1 = 9 };
+
+// Field byte offsets inside one weight block; -1 = field absent.
+template <int F> struct wfmt;
+template <> struct wfmt<FMT_Q4_0> { static constexpr int BB = 18, MOFF = -1, QH = -1, QS = 2; };
+template <> struct wfmt<FMT_Q4_1> { static constexpr int BB = 20, MOFF = 2, QH = -1, QS = 4; };
+template <> struct wfmt<FMT_Q5_0> { static constexpr int BB = 22, MOFF = -1, QH = 2, QS = 6; };
+template <> struct wfmt<FMT_Q5_1> { static constexpr int BB = 24, MOFF = 2, QH = 4, QS = 8; };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int QK = 32;
+constexpr int SB_BLOCKS = 8;        // blocks per super-block
+constexpr int SB_ELEMS = 256;       // elements per super-block
+constexpr int Q8_1_BYTES = 36;
+
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+
+template <int N> using ic = std::integral_constant<int, N>;
+template <int... Is, class Fn>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, Fn&& fn) {
+    (fn(ic<Is>{}), ...);
+}
+template <int N, class Fn> __device__ __forceinline__ void static_for(Fn&& fn) {
+    static_for_impl(std::make_integer_sequence<int, N>{}, fn);
+}
+
+// 32 bits starting at compile-time byte offset OFF of a register-resident byte stream.
+template <int OFF> __device__ __forceinline__ uint32_t ld32(const uint32_t* w) {
+    if constexpr (OFF % 4 == 0) return w[OFF / 4];
+    else return __builtin_amdgcn_alignbyte(w[OFF / 4 + 1], w[OFF / 4], OFF % 4);
+}
+// 16 bits at an even compile-time offset.
+template <int OFF> __device__ __forceinline__ uint32_t ld16(const uint32_t* w) {
+    static_assert(OFF % 2 == 0, "fp16 fields are 2-byte aligned");
+    if constexpr (OFF % 4 == 0) return w[OFF / 4] & 0xFFFFu;
+    else return w[OFF / 4] >> 16;
+}
+
+// Spread 4 bits (x in [0,15]) to bit 4 of each byte: bit k -> bit 8k+4. v_mul_u32_u24 is full rate.
+__device__ __forceinline__ uint32_t spread4_bit4(uint32_t x) {
+    return ((uint32_t)__umul24(x, 0x00204081u) & 0x01010101u) << 4;
+}
+
+// Decoded weight block: q[i] = elements 4i..4i+3 (i<4) / 16+4(i-4).. (i>=4) as unsigned bytes,
+// exactly the stored values (no offset removed), plus its scale(s).
+struct wblock {
+    uint32_t q[8];
+    float d, m;
+};
+
+// Decode block BI (0..7) of a register-resident super-block of format F.
+template <int F, int BI> __device__ __forceinline__ wblock decode_block(const uint32_t* w) {
+    using T = wfmt<F>;
+    constexpr int base = BI * T::BB;
+    wblock r;
+    r.d = h2f(ld16<base>(w));
+    if constexpr (T::MOFF >= 0) r.m = h2f(ld16<base + T::MOFF>(w));
+    else r.m = 0.0f;
+    uint32_t qh = 0;
+    if constexpr (T::QH >= 0) qh = ld32<base + T::QH>(w);
+    static_for<4>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t v = ld32<base + T::QS + 4 * i>(w);
+        uint32_t lo = v & 0x0F0F0F0Fu;
+        uint32_t hi = (v >> 4) & 0x0F0F0F0Fu;
+        if constexpr (T::QH >= 0) {
+            lo |= spread4_bit4((qh >> (4 * i)) & 0xFu);
+            hi |= spread4_bit4((qh >> (16 + 4 * i)) & 0xFu);
+        }
+        r.q[i] = lo;
+        r.q[4 + i] = hi;
+    });
+    return r;
+}
+
+// Integer dot of one decoded weight block with 8 activation dwords (elements 0..31 in order).
+__device__ __forceinline__ int dot_block(const uint32_t* q, const uint32_t* a) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = __builtin_amdgcn_sdot4((int)q[i], (int)a[i], s, false);
+    return s;
+}
+
+// Per-block fp32 term, operation order as in the reference (see header comment).
+template <int F> __device__ __forceinline__ float block_term(int sumi, float dw, float mw, float da, float sa) {
+    const float fs = (float)sumi;
+    if constexpr (F == FMT_Q4_0) return dw * (da * fs - 8.0f * sa);
+    else if constexpr (F == FMT_Q5_0) return dw * (da * fs - 16.0f * sa);
+    else return dw * da * fs + mw * sa;
+}
+
+}  // namespace qg

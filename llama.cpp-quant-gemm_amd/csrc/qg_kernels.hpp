@@ -1,0 +1,36 @@
+// qg_kernels.hpp — host-side view of the kernel families behind the C-ABI (qg_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qg {
+
+// One W4A8 product C = A_q8_1 * B_w^T, activation-major indices (m = activation row, n = weight
+// row); the output element (m, n) lives at C[m * ldc_m + n * ldc_n].
+struct GemmArgs {
+    const void* A = nullptr;     // block_q8_1 [M][K/32]
+    const void* B = nullptr;     // weight blocks [N][K/32] of type wtype
+    float* C = nullptr;
+    int32_t* sumi = nullptr;     // debug: per-block int32 dots [M][N][K/32] instead of C
+    int M = 0, N = 0, K = 0;
+    int wtype = 0;
+    long ldc_m = 0, ldc_n = 1;
+    bool nontemporal = true;     // weight stream loads with the nt hint
+};
+
+// GEMV / small batch (M <= 8), register-resident super-block decode + v_dot4.
+bool gemv_eligible(const GemmArgs& g);
+hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
+
+// Prefill (M > 8): LDS-staged activations, v_mfma_i32_32x32x32_i8 per Q-block.
+bool mfma_eligible(const GemmArgs& g);
+hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
+
+// Any shape / alignment with K % 32 == 0 (byte-granular loads); also the debug sumi fallback.
+hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
+
+// Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
+hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);
+hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st);
+
+}  // namespace qg

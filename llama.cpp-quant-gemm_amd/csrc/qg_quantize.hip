@@ -1,0 +1,248 @@
+// qg_quantize.hip — FP32 -> block quantizers and block -> FP32 dequantizers on gfx950.
+//
+// One thread per 32-element block, operation order and rounding exactly as the reference CPU
+// quantizers so the bytes are identical (roundf = round-half-away-from-zero, NOT the RNE
+// __float2int_rn of the reference's own GPU kernels, include/quantize.h:335; the division and the
+// reciprocal are IEEE-correct: the library builds with -fhip-fp32-correctly-rounded-divide-sqrt):
+//   Q8_1 (variant 0)  include/quantize.h:165-193  d = amax/127, s = sum(x) in element order
+//   Q8_1 (variant 1)  tests/framework/test_framework.cuh:195-225  s = d * sum(q), q clamped to +-127
+//   Q4_0              include/quantize.h:35-70     d = amax/7, q = clamp(roundf(x/d)+8, 0, 15)
+//   Q8_0              include/quantize.h:111-135
+//   Q4_1 / Q5_0 / Q5_1  tests/framework/test_framework.cuh:256-367 (the repo's only quantizers)
+#include "qg_common.hpp"
+#include "qg_kernels.hpp"
+
+namespace qg {
+
+__device__ __forceinline__ uint32_t f2h_bits(float f) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);  // RNE, as __float2half
+}
+
+template <bool VEC> __device__ __forceinline__ void load32(const float* __restrict__ x, float (&v)[32]) {
+    if constexpr (VEC) {
+        const float4* p = reinterpret_cast<const float4*>(x);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 t = p[i];
+            v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) v[i] = x[i];
+    }
+}
+
+// Store `nbytes` (even) bytes held little-endian in dwords w[] as 16-bit stores (blocks are only
+// 2-byte aligned inside AoS arrays).
+template <int NB> __device__ __forceinline__ void store_u16(uint8_t* dst, const uint32_t (&w)[(NB + 3) / 4]) {
+    uint16_t* p = reinterpret_cast<uint16_t*>(dst);
+#pragma unroll
+    for (int i = 0; i < NB / 2; ++i) p[i] = (uint16_t)(w[i / 2] >> (16 * (i & 1)));
+}
+
+template <int TYPE, int VARIANT, bool VEC>
+__global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__ x, uint8_t* __restrict__ y, int64_t nblocks) {
+    const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ib >= nblocks) return;
+    float v[32];
+    load32<VEC>(x + ib * QK, v);
+
+    if constexpr (TYPE == FMT_Q8_1 || TYPE == FMT_Q8_0) {
+        float amax = 0.0f, sum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            amax = fmaxf(amax, fabsf(v[j]));
+            sum += v[j];
+        }
+        const float d = amax / 127.0f;
+        const float id = d > 0.0f ? 1.0f / d : 0.0f;
+        uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int sq = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            int t = (int)roundf(v[j] * id);
+            t = VARIANT == 1 ? max(-127, min(127, t)) : max(-128, min(127, t));
+            sq += t;
+            q[j / 4] |= ((uint32_t)t & 0xFFu) << (8 * (j & 3));
+        }
+        if constexpr (TYPE == FMT_Q8_1) {
+            const float s = VARIANT == 1 ? (float)sq * d : sum;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);  // 36-B blocks stay 4-B aligned
+            dst[0] = f2h_bits(d) | (f2h_bits(s) << 16);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dst[1 + i] = q[i];
+        } else {
+            uint32_t w[9];
+            w[0] = f2h_bits(d) | ((q[0] & 0xFFFFu) << 16);
+#pragma unroll
+            for (int i = 1; i < 8; ++i) w[i] = (q[i - 1] >> 16) | ((q[i] & 0xFFFFu) << 16);
+            w[8] = q[7] >> 16;
+            store_u16<34>(y + ib * 34, w);
+        }
+    } else if constexpr (TYPE == FMT_Q4_0 || TYPE == FMT_Q5_0) {
+        float amax = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        constexpr float DIV = TYPE == FMT_Q4_0 ? 7.0f : 15.0f;
+        constexpr int OFF = TYPE == FMT_Q4_0 ? 8 : 16;
+        constexpr int QMAX = TYPE == FMT_Q4_0 ? 15 : 31;
+        const float d = amax / DIV;
+        const float id = d > 0.0f ? 1.0f / d : 0.0f;
+        uint8_t qs[16];
+        uint32_t qh = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            int q0 = (int)roundf(v[j] * id) + OFF;
+            int q1 = (int)roundf(v[j + 16] * id) + OFF;
+            q0 = max(0, min(QMAX, q0));
+            q1 = max(0, min(QMAX, q1));
+            qs[j] = (uint8_t)((q0 & 0xF) | ((q1 & 0xF) << 4));
+            qh |= (uint32_t)((q0 >> 4) & 1) << j;
+            qh |= (uint32_t)((q1 >> 4) & 1) << (j + 16);
+        }
+        if constexpr (TYPE == FMT_Q4_0) {
+            uint32_t w[5];
+            w[0] = f2h_bits(d) | ((uint32_t)qs[0] << 16) | ((uint32_t)qs[1] << 24);
+#pragma unroll
+            for (int i = 1; i < 4; ++i)
+                w[i] = (uint32_t)qs[4 * i - 2] | ((uint32_t)qs[4 * i - 1] << 8) | ((uint32_t)qs[4 * i] << 16) |
+                       ((uint32_t)qs[4 * i + 1] << 24);
+            w[4] = (uint32_t)qs[14] | ((uint32_t)qs[15] << 8);
+            store_u16<18>(y + ib * 18, w);
+        } else {
+            uint32_t w[6];
+            w[0] = f2h_bits(d) | ((qh & 0xFFFFu) << 16);
+            w[1] = (qh >> 16) | ((uint32_t)qs[0] << 16) | ((uint32_t)qs[1] << 24);
+#pragma unroll
+            for (int i = 2; i < 5; ++i)
+                w[i] = (uint32_t)qs[4 * i - 6] | ((uint32_t)qs[4 * i - 5] << 8) | ((uint32_t)qs[4 * i - 4] << 16) |
+                       ((uint32_t)qs[4 * i - 3] << 24);
+            w[5] = (uint32_t)qs[14] | ((uint32_t)qs[15] << 8);
+            store_u16<22>(y + ib * 22, w);
+        }
+    } else {  // Q4_1 / Q5_1: min/max, sequential compare from element 0 as the reference loop
+        float mn = v[0], mx = v[0];
+#pragma unroll
+        for (int j = 1; j < 32; ++j) {
+            if (v[j] < mn) mn = v[j];
+            if (v[j] > mx) mx = v[j];
+        }
+        constexpr float DIV = TYPE == FMT_Q4_1 ? 15.0f : 31.0f;
+        constexpr int QMAX = TYPE == FMT_Q4_1 ? 15 : 31;
+        const float d = (mx - mn) / DIV;
+        const float id = d > 0.0f ? 1.0f / d : 0.0f;
+        uint8_t qs[16];
+        uint32_t qh = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            int q0 = (int)roundf((v[j] - mn) * id);
+            int q1 = (int)roundf((v[j + 16] - mn) * id);
+            q0 = max(0, min(QMAX, q0));
+            q1 = max(0, min(QMAX, q1));
+            qs[j] = (uint8_t)((q0 & 0xF) | ((q1 & 0xF) << 4));
+            qh |= (uint32_t)((q0 >> 4) & 1) << j;
+            qh |= (uint32_t)((q1 >> 4) & 1) << (j + 16);
+        }
+        const uint32_t dm = f2h_bits(d) | (f2h_bits(mn) << 16);
+        if constexpr (TYPE == FMT_Q4_1) {
+            uint32_t w[5];
+            w[0] = dm;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[1 + i] = (uint32_t)qs[4 * i] | ((uint32_t)qs[4 * i + 1] << 8) | ((uint32_t)qs[4 * i + 2] << 16) |
+                           ((uint32_t)qs[4 * i + 3] << 24);
+            store_u16<20>(y + ib * 20, w);
+        } else {
+            uint32_t w[6];
+            w[0] = dm;
+            w[1] = qh;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[2 + i] = (uint32_t)qs[4 * i] | ((uint32_t)qs[4 * i + 1] << 8) | ((uint32_t)qs[4 * i + 2] << 16) |
+                           ((uint32_t)qs[4 * i + 3] << 24);
+            store_u16<24>(y + ib * 24, w);
+        }
+    }
+}
+
+// Dequantize: x = (q - off) * d  or  q * d + m  (include/quantize.h:84-102, 140-150, 198-210).
+template <int TYPE>
+__global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, int64_t nblocks) {
+    const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ib >= nblocks) return;
+    float* o = y + ib * QK;
+    if constexpr (TYPE == FMT_Q8_0 || TYPE == FMT_Q8_1) {
+        constexpr int BB = TYPE == FMT_Q8_0 ? 34 : 36;
+        constexpr int QO = TYPE == FMT_Q8_0 ? 2 : 4;
+        const uint8_t* b = x + ib * BB;
+        const float d = h2f((uint32_t)b[0] | ((uint32_t)b[1] << 8));
+#pragma unroll
+        for (int j = 0; j < 32; ++j) o[j] = (float)(int8_t)b[QO + j] * d;
+    } else {
+        using T = wfmt<TYPE>;
+        const uint8_t* b = x + ib * T::BB;
+        const float d = h2f((uint32_t)b[0] | ((uint32_t)b[1] << 8));
+        float m = 0.0f;
+        if constexpr (T::MOFF >= 0) m = h2f((uint32_t)b[T::MOFF] | ((uint32_t)b[T::MOFF + 1] << 8));
+        uint32_t qh = 0;
+        if constexpr (T::QH >= 0)
+            qh = (uint32_t)b[T::QH] | ((uint32_t)b[T::QH + 1] << 8) | ((uint32_t)b[T::QH + 2] << 16) |
+                 ((uint32_t)b[T::QH + 3] << 24);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            int q0 = b[T::QS + j] & 0xF, q1 = b[T::QS + j] >> 4;
+            if constexpr (T::QH >= 0) {
+                q0 |= (int)((qh >> j) & 1u) << 4;
+                q1 |= (int)((qh >> (j + 16)) & 1u) << 4;
+            }
+            if constexpr (TYPE == FMT_Q4_0) { o[j] = (float)(q0 - 8) * d; o[j + 16] = (float)(q1 - 8) * d; }
+            else if constexpr (TYPE == FMT_Q5_0) { o[j] = (float)(q0 - 16) * d; o[j + 16] = (float)(q1 - 16) * d; }
+            else { o[j] = (float)q0 * d + m; o[j + 16] = (float)q1 * d + m; }
+        }
+    }
+}
+
+namespace {
+template <int TYPE, int VARIANT>
+hipError_t lq(const float* x, void* y, int64_t nblocks, hipStream_t st) {
+    const dim3 grid((unsigned)((nblocks + 255) / 256));
+    if (((uintptr_t)x & 15) == 0)
+        hipLaunchKernelGGL((quantize_kernel<TYPE, VARIANT, true>), grid, dim3(256), 0, st, x, (uint8_t*)y, nblocks);
+    else
+        hipLaunchKernelGGL((quantize_kernel<TYPE, VARIANT, false>), grid, dim3(256), 0, st, x, (uint8_t*)y, nblocks);
+    return hipGetLastError();
+}
+template <int TYPE> hipError_t ld(const void* x, float* y, int64_t nblocks, hipStream_t st) {
+    hipLaunchKernelGGL((dequantize_kernel<TYPE>), dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, st,
+                       (const uint8_t*)x, y, nblocks);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st) {
+    if (nblocks == 0) return hipSuccess;
+    switch (type) {
+        case FMT_Q8_1: return variant == 1 ? lq<FMT_Q8_1, 1>(x, y, nblocks, st) : lq<FMT_Q8_1, 0>(x, y, nblocks, st);
+        case FMT_Q8_0: return lq<FMT_Q8_0, 0>(x, y, nblocks, st);
+        case FMT_Q4_0: return lq<FMT_Q4_0, 0>(x, y, nblocks, st);
+        case FMT_Q4_1: return lq<FMT_Q4_1, 0>(x, y, nblocks, st);
+        case FMT_Q5_0: return lq<FMT_Q5_0, 0>(x, y, nblocks, st);
+        case FMT_Q5_1: return lq<FMT_Q5_1, 0>(x, y, nblocks, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st) {
+    if (nblocks == 0) return hipSuccess;
+    switch (type) {
+        case FMT_Q8_1: return ld<FMT_Q8_1>(x, y, nblocks, st);
+        case FMT_Q8_0: return ld<FMT_Q8_0>(x, y, nblocks, st);
+        case FMT_Q4_0: return ld<FMT_Q4_0>(x, y, nblocks, st);
+        case FMT_Q4_1: return ld<FMT_Q4_1>(x, y, nblocks, st);
+        case FMT_Q5_0: return ld<FMT_Q5_0>(x, y, nblocks, st);
+        case FMT_Q5_1: return ld<FMT_Q5_1>(x, y, nblocks, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace qg

@@ -1,0 +1,194 @@
+"""quant_gemm — MI355X (gfx950) W4A8 quantized GEMM, drop-in for the reference's Python face.
+
+Same names, argument meaning, tensor layouts and error behaviour as the reference package
+(python/quant_gemm/__init__.py:33-89, python/quant_gemm/csrc/bindings.cpp:19-91):
+
+    weight_q     = quant_gemm.quantize_q4_0(weight)        # f32 [..., K] -> u8 [..., K/32, 18]
+    activation_q = quant_gemm.quantize_q8_1(activation)    # f32 [..., K] -> u8 [..., K/32, 36]
+    out = quant_gemm.gemm_q4_0_q8_1(weight_q, activation_q, M, N, K)   # f32 [M, N] (weight-major)
+    x   = quant_gemm.dequantize_q4_0(weight_q, K)
+
+Differences, all deliberate: kernels run on torch's *current* HIP stream (the reference launches
+on the legacy default stream, gemm_ops.cu:250); validation errors raise RuntimeError like
+TORCH_CHECK does. Extra entry points expose the rest of the C-ABI: the activation-major
+``gemm_w4a8`` (include/gemm_reference.h convention), Q4_1/Q5_0/Q5_1 weights, every quantizer and
+the per-block ``debug_sumi`` parity hook. Every call goes to HIP kernels in ``libqg_hip.so``;
+there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+__version__ = "0.1.0"
+
+QK4_0 = 32
+QK8_1 = 32
+BLOCK_Q4_0_BYTES = 18
+BLOCK_Q8_1_BYTES = 36
+
+# ggml_type ids (compat/ggml_types.h:199-215)
+Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1 = 2, 3, 6, 7, 8, 9
+BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q5_0: 22, Q5_1: 24, Q8_0: 34, Q8_1: 36}
+ALGO_AUTO, ALGO_GEMV, ALGO_MFMA, ALGO_GENERIC = 0, 1, 2, 3
+
+
+def _require(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _stream(dev: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# ---------------------------------------------------------------------------- quantizers
+def quantize(x: torch.Tensor, qtype: int, variant: int = 0) -> torch.Tensor:
+    """FP32 [..., K] -> uint8 [..., K/32, block_bytes(qtype)], bytes identical to the reference
+    CPU quantizers (include/quantize.h; tests/framework/test_framework.cuh for Q4_1/Q5_x and
+    Q8_1 variant 1)."""
+    _require(x.is_cuda, "Input must be a CUDA tensor")
+    _require(x.dtype == torch.float32, "Input must be float32")
+    _require(x.dim() >= 1, "Input must have at least 1 dimension")
+    K = x.size(-1)
+    _require(K % 32 == 0, f"Last dimension must be divisible by 32, got {K}")
+    _require(qtype in BLOCK_BYTES, f"unknown quant type {qtype}")
+    x = x.contiguous()
+    out = torch.empty(tuple(x.shape[:-1]) + (K // 32, BLOCK_BYTES[qtype]), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.load().qg_quantize(qtype, variant, _ptr(x), _ptr(out), x.numel(), _stream(x.device)),
+                   "quantize")
+    return out
+
+
+def quantize_q4_0(x: torch.Tensor) -> torch.Tensor:
+    """Quantize FP32 tensor to Q4_0: [..., K] -> uint8 [..., K//32, 18]."""
+    return quantize(x, Q4_0)
+
+
+def quantize_q8_1(x: torch.Tensor) -> torch.Tensor:
+    """Quantize FP32 tensor to Q8_1: [..., K] -> uint8 [..., K//32, 36]."""
+    return quantize(x, Q8_1)
+
+
+def dequantize(x_q: torch.Tensor, qtype: int) -> torch.Tensor:
+    _require(x_q.is_cuda, "Input must be a CUDA tensor")
+    _require(x_q.dtype == torch.uint8, "Input must be uint8")
+    _require(qtype in BLOCK_BYTES, f"unknown quant type {qtype}")
+    bb = BLOCK_BYTES[qtype]
+    _require(x_q.numel() % bb == 0, f"Input size {x_q.numel()} is not a multiple of {bb}-byte blocks")
+    x_q = x_q.contiguous()
+    nblocks = x_q.numel() // bb
+    shape = tuple(x_q.shape[:-2]) + (x_q.shape[-2] * 32,) if x_q.dim() >= 2 else (nblocks * 32,)
+    out = torch.empty(shape, dtype=torch.float32, device=x_q.device)
+    with torch.cuda.device(x_q.device):
+        _lib.check(_lib.load().qg_dequantize(qtype, _ptr(x_q), _ptr(out), nblocks * 32, _stream(x_q.device)),
+                   "dequantize")
+    return out
+
+
+def dequantize_q4_0(x_q: torch.Tensor, K: int) -> torch.Tensor:
+    """Dequantize Q4_0 [..., K//32, 18] back to FP32 [..., K]."""
+    _require(x_q.is_cuda, "Input must be a CUDA tensor")
+    _require(x_q.dtype == torch.uint8, "Input must be uint8")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    out = dequantize(x_q, Q4_0)
+    return out.reshape(tuple(x_q.shape[:-2]) + (K,))
+
+
+# ---------------------------------------------------------------------------- GEMMs
+def _check_blocks(t: torch.Tensor, what: str, rows: int, K: int, bb: int) -> None:
+    _require(t.is_cuda, f"{what} must be a CUDA tensor")
+    _require(t.dtype == torch.uint8, f"{what} must be uint8")
+    expect = rows * (K // 32) * bb
+    _require(t.numel() == expect, f"{what} shape mismatch: expected {expect} elements, got {t.numel()}")
+
+
+def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
+              wtype: int = Q4_0, algo: int = ALGO_AUTO, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Activation-major C[M, N] = A_q8_1[M, K] . B_w[N, K]^T (include/gemm_reference.h:175-222;
+    include/llama_adapter.h). M = tokens, N = weight rows."""
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(wtype in (Q4_0, Q4_1, Q5_0, Q5_1), f"unsupported weight type {wtype}")
+    _check_blocks(activation_q, "Activation", M, K, 36)
+    _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
+    a = activation_q.contiguous()
+    w = weight_q.contiguous()
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=w.device)
+    else:
+        _require(out.is_contiguous() and out.dtype == torch.float32 and out.numel() == M * N, "bad out tensor")
+    with torch.cuda.device(w.device):
+        _lib.check(_lib.load().qg_gemm_w4a8_ex(_ptr(a), _ptr(w), _ptr(out), M, N, K, wtype, algo,
+                                               _stream(w.device)), "gemm_w4a8")
+    return out
+
+
+def _gemm_weight_major(sym: str, wtype: int, weight_q, activation_q, M, N, K):
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _check_blocks(weight_q, "Weight", M, K, BLOCK_BYTES[wtype])
+    _check_blocks(activation_q, "Activation", N, K, 36)
+    w = weight_q.contiguous()
+    a = activation_q.contiguous()
+    out = torch.empty((M, N), dtype=torch.float32, device=w.device)
+    with torch.cuda.device(w.device):
+        _lib.check(getattr(_lib.load(), sym)(_ptr(w), _ptr(a), _ptr(out), M, N, K, _stream(w.device)), sym)
+    return out
+
+
+def gemm_q4_0_q8_1(weight_q: torch.Tensor, activation_q: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """Quantized GEMM C[M,N] = W[M,K] @ A[N,K]^T (weight-major: M = weight rows, N = tokens).
+
+    weight_q: uint8 [M, K//32, 18]; activation_q: uint8 [N, K//32, 36]; returns f32 [M, N]."""
+    return _gemm_weight_major("qg_gemm_q4_0_q8_1", Q4_0, weight_q, activation_q, M, N, K)
+
+
+def gemm_q4_1_q8_1(weight_q, activation_q, M: int, N: int, K: int) -> torch.Tensor:
+    return _gemm_weight_major("qg_gemm_q4_1_q8_1", Q4_1, weight_q, activation_q, M, N, K)
+
+
+def gemm_q5_0_q8_1(weight_q, activation_q, M: int, N: int, K: int) -> torch.Tensor:
+    return _gemm_weight_major("qg_gemm_q5_0_q8_1", Q5_0, weight_q, activation_q, M, N, K)
+
+
+def gemm_q5_1_q8_1(weight_q, activation_q, M: int, N: int, K: int) -> torch.Tensor:
+    return _gemm_weight_major("qg_gemm_q5_1_q8_1", Q5_1, weight_q, activation_q, M, N, K)
+
+
+def debug_sumi(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
+               wtype: int = Q4_0, algo: int = ALGO_AUTO) -> torch.Tensor:
+    """Per-block int32 dots [M, N, K/32] through the same decode path as ``algo``."""
+    _check_blocks(activation_q, "Activation", M, K, 36)
+    _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
+    out = torch.empty((M, N, K // 32), dtype=torch.int32, device=weight_q.device)
+    with torch.cuda.device(weight_q.device):
+        _lib.check(_lib.load().qg_debug_sumi(_ptr(activation_q.contiguous()), _ptr(weight_q.contiguous()),
+                                             _ptr(out), M, N, K, wtype, algo, _stream(weight_q.device)),
+                   "debug_sumi")
+    return out
+
+
+def select_algo(M: int, N: int, K: int, wtype: int = Q4_0) -> int:
+    return _lib.load().qg_select_algo(M, N, K, wtype)
+
+
+def version() -> str:
+    return _lib.load().qg_version().decode()
+
+
+_lib.load()  # fail loudly at import if the HIP library is absent
+
+__all__ = [
+    "quantize_q4_0", "quantize_q8_1", "gemm_q4_0_q8_1", "dequantize_q4_0",
+    "QK4_0", "QK8_1", "BLOCK_Q4_0_BYTES", "BLOCK_Q8_1_BYTES",
+    "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
+    "debug_sumi", "select_algo", "version",
+    "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
+]

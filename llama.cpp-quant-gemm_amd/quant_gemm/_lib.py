@@ -1,0 +1,69 @@
+"""Loader for the in-tree HIP library ``libqg_hip.so`` (C-ABI: include/qg/qg.h).
+
+There is no fallback: if the library is missing or does not load, importing ``quant_gemm``
+raises. ``torch`` is imported first so the library binds to the HIP runtime torch already loaded
+(both carry SONAME libamdhip64.so.7) — one runtime per process, torch's streams valid in ours.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqg_hip.so")
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+
+QG_OK = 0
+STATUS = {0: "ok", -1: "invalid argument", -2: "K must be a positive multiple of 32",
+          -3: "unsupported type or algorithm for this shape", -4: "pointer misaligned for the block format",
+          -5: "HIP launch error"}
+
+# exported symbols and their signatures (kept in sync with include/qg/qg.h; tests check both ways)
+P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+SIGNATURES = {
+    "qg_gemm_w4a8": ([P, P, P, I, I, I, I, P], I),
+    "qg_gemm_w4a8_ex": ([P, P, P, I, I, I, I, I, P], I),
+    "qg_gemm_q4_0_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q5_0_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q5_1_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_quantize_q8_1": ([P, P, I64, P], I),
+    "qg_quantize_q4_0": ([P, P, I64, P], I),
+    "qg_quantize": ([I, I, P, P, I64, P], I),
+    "qg_dequantize": ([I, P, P, I64, P], I),
+    "qg_dequantize_q4_0": ([P, P, I64, P], I),
+    "qg_debug_sumi": ([P, P, P, I, I, I, I, I, P], I),
+    "qg_gemm_w4a8_from_view": ([P, P, P, ctypes.c_char_p, P], I),
+    "qg_status_string": ([I], ctypes.c_char_p),
+    "qg_last_hip_error": ([], I),
+    "qg_select_algo": ([I, I, I, I], I),
+    "qg_block_bytes": ([I], I),
+    "qg_version": ([], ctypes.c_char_p),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"quant_gemm: HIP library not built ({LIB_PATH}); run `make -C {CSRC}` "
+                              "or __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != QG_OK:
+        extra = ""
+        if status == -5:
+            extra = f" (hipError {load().qg_last_hip_error()})"
+        raise RuntimeError(f"{what}: {STATUS.get(status, status)}{extra}")

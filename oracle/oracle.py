@@ -1,0 +1,185 @@
+"""CPU oracle for the W4A8 path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker (or the timed CPU baseline). The product path
+(``quant_gemm`` over ``libqg_hip.so``) never imports it and has no CPU fallback.
+
+It wraps ``_build/libqg_oracle.so`` (``qg_oracle.c``: an operation-for-operation C restatement
+of the reference's CPU ground truth, see the file:line table in its header) with numpy
+conveniences. Pinning (``tests/test_oracle.py``):
+  * known-answer values held in the reference's own files (TEST_RESULTS.md:113-119, the
+    test_cpu_ref.cpp / test_dot.cpp / test_q8_1.cpp programs compiled from the reference tree
+    into ``_ref/``, test_dp4a.cu:24-48);
+  * golden vectors produced by the reference's runnable Python definitions
+    (flashinfer_trace/definitions/**.json ``reference``) via tests/golden/make_golden.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libqg_oracle.so")
+
+Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1 = 2, 3, 6, 7, 8, 9
+BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q5_0: 22, Q5_1: 24, Q8_0: 34, Q8_1: 36}
+TYPE_NAMES = {Q4_0: "q4_0", Q4_1: "q4_1", Q5_0: "q5_0", Q5_1: "q5_1", Q8_0: "q8_0", Q8_1: "q8_1"}
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, I64, U = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint
+        L.qgo_fill_uniform_step4.argtypes = [U, P, I64, P, I64]
+        for name in ("qgo_quantize_row_q4_0", "qgo_quantize_row_q8_0", "qgo_quantize_row_q8_1",
+                     "qgo_quantize_q8_1_fw", "qgo_quantize_q4_1", "qgo_quantize_q5_0", "qgo_quantize_q5_1"):
+            getattr(L, name).argtypes = [P, P, I64]
+        L.qgo_dequantize.argtypes = [I, P, P, I64]
+        L.qgo_gemm_fp32.argtypes = [P, P, P, I, I, I]
+        L.qgo_gemm_w4a16.argtypes = [P, P, P, I, I, I]
+        L.qgo_gemm_w4a8.argtypes = [P, P, P, P, I, I, I, I]
+        L.qgo_gemm_w4a8_mt.argtypes = [P, P, P, I, I, I, I, I]
+        L.qgo_gemm_w8a8.argtypes = [P, P, P, I, I, I]
+        L.qgo_vec_dot_q4_0_q8_1.argtypes = [I, P, P, P]
+        L.qgo_dot4.argtypes = [ctypes.c_int32] * 3
+        L.qgo_dot4.restype = ctypes.c_int32
+        L.qgo_f2h.argtypes = [ctypes.c_float]
+        L.qgo_f2h.restype = ctypes.c_uint16
+        L.qgo_h2f.argtypes = [ctypes.c_uint16]
+        L.qgo_h2f.restype = ctypes.c_float
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray) -> ctypes.c_void_p:
+    assert a.flags["C_CONTIGUOUS"]
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def fill_uniform_step4(m: int, n: int, k: int, seed: int = 42):
+    """A[m,k], B[n,k] ~ U[-1,1] from glibc srand(seed)/rand(), A first (tests/step4_w4a8_gemm.cu:142-148)."""
+    a = np.empty((m, k), np.float32)
+    b = np.empty((n, k), np.float32)
+    lib().qgo_fill_uniform_step4(seed, _p(a), a.size, _p(b), b.size)
+    return a, b
+
+
+_QUANT = {Q4_0: "qgo_quantize_row_q4_0", Q8_0: "qgo_quantize_row_q8_0", Q8_1: "qgo_quantize_row_q8_1",
+          Q4_1: "qgo_quantize_q4_1", Q5_0: "qgo_quantize_q5_0", Q5_1: "qgo_quantize_q5_1"}
+
+
+def quantize(x: np.ndarray, t: int, variant: int = 0) -> np.ndarray:
+    """FP32 [..., K] -> uint8 [..., K/32, block_bytes] (reference CPU quantizers)."""
+    x = np.ascontiguousarray(x, np.float32)
+    k = x.shape[-1]
+    assert k % 32 == 0
+    out = np.empty(x.shape[:-1] + (k // 32, BLOCK_BYTES[t]), np.uint8)
+    fn = "qgo_quantize_q8_1_fw" if (t == Q8_1 and variant == 1) else _QUANT[t]
+    getattr(lib(), fn)(_p(x), _p(out), x.size)
+    return out
+
+
+def dequantize(q: np.ndarray, t: int) -> np.ndarray:
+    q = np.ascontiguousarray(q, np.uint8)
+    k = q.shape[-2] * 32
+    out = np.empty(q.shape[:-2] + (k,), np.float32)
+    lib().qgo_dequantize(t, _p(q), _p(out), out.size)
+    return out
+
+
+def gemm_fp32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    m, k = a.shape
+    n = b.shape[0]
+    c = np.empty((m, n), np.float32)
+    lib().qgo_gemm_fp32(_p(a), _p(b), _p(c), m, n, k)
+    return c
+
+
+def gemm_w4a8(a_q: np.ndarray, b_q: np.ndarray, t: int = Q4_0, want_sumi: bool = False):
+    """C[M,N] (and optionally sumi[M,N,K/32]) — include/gemm_reference.h:175-222 semantics."""
+    a_q = np.ascontiguousarray(a_q, np.uint8)
+    b_q = np.ascontiguousarray(b_q, np.uint8)
+    m, nb = a_q.shape[0], a_q.shape[1]
+    n = b_q.shape[0]
+    assert a_q.shape[2] == 36 and b_q.shape[1] == nb and b_q.shape[2] == BLOCK_BYTES[t]
+    c = np.empty((m, n), np.float32)
+    s = np.empty((m, n, nb), np.int32) if want_sumi else None
+    lib().qgo_gemm_w4a8(_p(a_q), _p(b_q), _p(c), _p(s) if want_sumi else None, m, n, nb * 32, t)
+    return (c, s) if want_sumi else c
+
+
+def gemm_w4a8_mt(a_q, b_q, t: int = Q4_0, nthreads: int = 1) -> np.ndarray:
+    m, nb = a_q.shape[0], a_q.shape[1]
+    n = b_q.shape[0]
+    c = np.empty((m, n), np.float32)
+    lib().qgo_gemm_w4a8_mt(_p(a_q), _p(b_q), _p(c), m, n, nb * 32, t, nthreads)
+    return c
+
+
+def gemm_w4a16(a: np.ndarray, b_q: np.ndarray) -> np.ndarray:
+    m, k = a.shape
+    n = b_q.shape[0]
+    c = np.empty((m, n), np.float32)
+    lib().qgo_gemm_w4a16(_p(np.ascontiguousarray(a, np.float32)), _p(b_q), _p(c), m, n, k)
+    return c
+
+
+def vec_dot_q4_0_q8_1(x_q4: np.ndarray, y_q8: np.ndarray) -> float:
+    s = ctypes.c_float()
+    n = x_q4.reshape(-1, 18).shape[0] * 32
+    lib().qgo_vec_dot_q4_0_q8_1(n, ctypes.byref(s), _p(np.ascontiguousarray(x_q4)), _p(np.ascontiguousarray(y_q8)))
+    return s.value
+
+
+def dot4(a: int, b: int, c: int = 0) -> int:
+    return lib().qgo_dot4(ctypes.c_int32(a), ctypes.c_int32(b), ctypes.c_int32(c))
+
+
+def nmse(out: np.ndarray, ref: np.ndarray) -> float:
+    """Sum e^2 / sum ref^2 in fp64 (tests/framework/test_framework.cuh:41-64)."""
+    out = np.asarray(out, np.float64)
+    ref = np.asarray(ref, np.float64)
+    den = float(np.sum(ref * ref))
+    num = float(np.sum((out - ref) ** 2))
+    return num / den if den > 0 else (0.0 if num == 0 else float("inf"))
+
+
+def _h(x: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(x).view(np.float16).astype(np.float32)[..., 0]
+
+
+def block_terms(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_0) -> np.ndarray:
+    """fp32 per-block terms [M,N,nb] in the reference's operation order (numpy fp32, no FMA)."""
+    da = _h(a_q[..., 0:2])[:, None, :]
+    sa = _h(a_q[..., 2:4])[:, None, :]
+    dw = _h(b_q[..., 0:2])[None, :, :]
+    fs = sumi.astype(np.float32)
+    if t == Q4_0:
+        return dw * (da * fs - np.float32(8.0) * sa)
+    if t == Q5_0:
+        return dw * (da * fs - np.float32(16.0) * sa)
+    mw = _h(b_q[..., 2:4])[None, :, :]
+    return dw * da * fs + mw * sa
+
+
+def summation_tol(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_0) -> np.ndarray:
+    """Bound on |fl(sum_b term_b) - fl'(sum_b term_b)| for any two fp32 summation orders
+    (2 * nb * 2^-24 * sum_b |term_b|) — the only legitimate CPU/GPU difference once the
+    per-block terms are bit-identical."""
+    terms = block_terms(a_q, b_q, sumi, t).astype(np.float64)
+    nb = terms.shape[-1]
+    return 2.0 * nb * 2.0 ** -24 * np.abs(terms).sum(axis=-1) + 1e-30

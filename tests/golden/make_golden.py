@@ -1,0 +1,89 @@
+"""Generate the golden fixtures under tests/golden/ (run in the build container only).
+
+Inputs come from the CPU oracle's restatement of the reference's input recipe (glibc srand(42),
+A then B ~ U[-1,1], tests/step4_w4a8_gemm.cu:142-148) and quantizers (include/quantize.h). The
+EXPECTED outputs come from the reference itself: the runnable Python ``reference`` definitions
+shipped in /root/reference/flashinfer_trace/definitions/ (read at generation time, executed here,
+never copied into this repo):
+
+  quant_gemm/w4a8_q4_0_q8_1_n4096_k4096.json     -> W4A8 Q4_0 outputs  (json "reference", :77)
+  quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json   -> W4A8 Q4_1 outputs  (:79)
+  quantize/quantize_q8_1_k4096.json              -> Q8_1 bytes         (:66)
+
+The reference tree does not exist on the GPU box; the tests only read the .npz written here.
+Usage:  python tests/golden/make_golden.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle as O  # noqa: E402
+
+
+def load_reference_fn(ref_root: str, rel: str, fn: str = "run"):
+    with open(os.path.join(ref_root, "flashinfer_trace", "definitions", rel)) as f:
+        spec = json.load(f)
+    ns: dict = {}
+    exec(compile(spec["reference"], rel, "exec"), ns)  # the reference's own Python definition
+    return ns[fn]
+
+
+def as_block_objects(q: np.ndarray) -> np.ndarray:
+    """uint8 [rows, nb, bytes] -> object [rows, nb] of `bytes` (the definitions' input contract)."""
+    rows, nb, _ = q.shape
+    out = np.empty((rows, nb), dtype=object)
+    for r in range(rows):
+        for b in range(nb):
+            out[r, b] = bytes(q[r, b].tobytes())
+    return out
+
+
+def w4a8_case(run, m, n, k, wtype, seed=42):
+    a, b = O.fill_uniform_step4(m, n, k, seed)
+    a_q = O.quantize(a, O.Q8_1)
+    b_q = O.quantize(b, wtype)
+    c_ref = run(as_block_objects(a_q), as_block_objects(b_q)).numpy().astype(np.float32)
+    return dict(m=np.int32(m), n=np.int32(n), k=np.int32(k), seed=np.int32(seed), wtype=np.int32(wtype),
+                a_q=a_q, b_q=b_q, c_ref=c_ref, a_head=a[0, :8].copy(), b_head=b[0, :8].copy(),
+                c_fp32=O.gemm_fp32(a, b))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+
+    run_q4_0 = load_reference_fn(args.ref, "quant_gemm/w4a8_q4_0_q8_1_n4096_k4096.json")
+    run_q4_1 = load_reference_fn(args.ref, "quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json")
+    quant_q8_1 = load_reference_fn(args.ref, "quantize/quantize_q8_1_k4096.json", "quantize_block_q8_1")
+
+    cases = {
+        # BASELINE.json configs[0]: the plumbing config, in full
+        "w4a8_q4_0_plumbing": w4a8_case(run_q4_0, 1, 128, 256, O.Q4_0),
+        "w4a8_q4_0_m2n8k128": w4a8_case(run_q4_0, 2, 8, 128, O.Q4_0),
+        "w4a8_q4_0_m3n5k96": w4a8_case(run_q4_0, 3, 5, 96, O.Q4_0, seed=7),
+        "w4a8_q4_1_m2n8k128": w4a8_case(run_q4_1, 2, 8, 128, O.Q4_1),
+        "w4a8_q4_1_m1n16k256": w4a8_case(run_q4_1, 1, 16, 256, O.Q4_1, seed=3),
+    }
+    for name, d in cases.items():
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
+        print(f"{name}: C[0,:4]={d['c_ref'].ravel()[:4]}")
+
+    # Q8_1 quantizer: the definition's own bytes for 16 rows x 4 blocks of the step4 A stream.
+    a, _ = O.fill_uniform_step4(16, 0, 128, 42)
+    blocks = np.stack([np.frombuffer(quant_q8_1(a[r, 32 * j:32 * j + 32]), np.uint8)
+                       for r in range(16) for j in range(4)]).reshape(16, 4, 36)
+    np.savez_compressed(os.path.join(HERE, "quantize_q8_1_m16k128.npz"), x=a, q_ref=blocks)
+    print("quantize_q8_1: ok")
+
+
+if __name__ == "__main__":
+    main()

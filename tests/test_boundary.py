@@ -1,0 +1,129 @@
+"""The C-ABI drop-in boundary (include/qg/qg.h) — CPU-only checks, no kernel launches.
+
+* libqg_hip.so loads and exports every function include/qg/qg.h declares (and the Python mirror
+  binds exactly those);
+* argument validation returns the documented status codes before anything is enqueued
+  (the reference's wrappers validate nothing, include/gemm_cuda_naive.cuh:285-292; its Python face
+  raises via TORCH_CHECK, python/quant_gemm/csrc/bindings.cpp:19-70);
+* the Python mirror's error messages match the reference's TORCH_CHECK texts.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "qg", "qg.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(qg_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import quant_gemm._lib as L
+    return L
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for must in ("qg_gemm_w4a8", "qg_gemm_q4_0_q8_1", "qg_quantize_q8_1", "qg_quantize_q4_0",
+                 "qg_dequantize_q4_0", "qg_gemm_w4a8_from_view", "qg_debug_sumi"):
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol(lib):
+    so = lib.load()
+    fns = declared_functions()
+    for f in fns:
+        assert hasattr(so, f), f
+    nm = subprocess.run(["nm", "-D", "--defined-only", lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (qg_\w+)", nm))
+    assert set(fns) <= exported
+    assert set(lib.SIGNATURES) == set(fns), "Python bindings out of sync with qg.h"
+
+
+def test_library_is_gfx950_code_object(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib.LIB_PATH],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout
+
+
+def test_static_queries(lib):
+    so = lib.load()
+    assert so.qg_version().decode().startswith("qg-mi355x")
+    assert [so.qg_block_bytes(t) for t in (2, 3, 6, 7, 8, 9, 0)] == [18, 20, 22, 24, 34, 36, 0]
+    assert so.qg_select_algo(1, 4096, 4096, 2) == 1      # decode -> GEMV
+    assert so.qg_select_algo(8, 4096, 4096, 6) == 1
+    assert so.qg_select_algo(1, 4096, 4128, 2) == 3      # K % 256 != 0 -> generic
+    assert so.qg_select_algo(1, 4096, 33, 2) == -1
+    assert so.qg_status_string(-2).decode().startswith("K must be")
+
+
+def test_validation_codes_without_launch(lib):
+    so = lib.load()
+    P = ctypes.c_void_p
+    fake = P(4096)  # never dereferenced: validation fails first
+    assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 33, 2, None) == -2        # bad K
+    assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 0, 2, None) == -2
+    assert so.qg_gemm_w4a8(fake, fake, fake, -1, 1, 32, 2, None) == -1       # negative M
+    assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 32, 8, None) == -3        # Q8_0 weights: not on this path
+    assert so.qg_gemm_w4a8(None, fake, fake, 1, 1, 32, 2, None) == -1        # null
+    assert so.qg_gemm_w4a8(None, None, None, 0, 5, 64, 2, None) == 0         # empty: no-op
+    assert so.qg_gemm_w4a8(fake, P(4097), fake, 1, 1, 32, 2, None) == -4     # odd weight pointer
+    assert so.qg_gemm_w4a8_ex(fake, fake, fake, 1, 1, 288, 2, 1, None) == -3  # GEMV needs K % 256 == 0
+    assert so.qg_quantize(2, 0, fake, fake, 33, None) == -2
+    assert so.qg_quantize(2, 1, fake, fake, 32, None) == -3                  # variant 1 is Q8_1 only
+    assert so.qg_quantize(9, 0, P(4098), fake, 32, None) == -4               # float input misaligned
+    assert so.qg_quantize(9, 0, fake, P(4098), 32, None) == -4               # Q8_1 blocks need 4-B alignment
+    assert so.qg_quantize(9, 0, None, None, 0, None) == 0
+    assert so.qg_dequantize(5, fake, fake, 32, None) == -3
+
+
+def test_from_view_validation(lib):
+    so = lib.load()
+
+    class View(ctypes.Structure):
+        _fields_ = [("data", ctypes.c_void_p), ("type", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
+                    ("nb", ctypes.c_size_t * 4)]
+
+    def view(t, ne0, ne1, bb):
+        v = View()
+        v.data, v.type = 4096, t
+        v.ne[:] = [ne0, ne1, 1, 1]
+        row = (ne0 // 32) * bb if t != 0 else ne0 * 4
+        v.nb[:] = [bb if t != 0 else 4, row, row * ne1, row * ne1]
+        return v
+
+    act, w = view(9, 4096, 1, 36), view(2, 4096, 8, 18)
+    out = View()
+    out.data, out.type = 4096, 0
+    out.ne[:] = [8, 1, 1, 1]
+    out.nb[:] = [4, 32, 32, 32]
+    p = ctypes.byref
+    assert so.qg_gemm_w4a8_from_view(p(act), p(w), p(out), b"bogus", None) == -1
+    bad = View()
+    ctypes.pointer(bad)[0] = out
+    bad.type = 2
+    assert so.qg_gemm_w4a8_from_view(p(act), p(w), p(bad), b"naive", None) == -3  # output must be F32
+    assert so.qg_gemm_w4a8_from_view(p(act), p(act), p(out), b"naive", None) == -3  # Q8_1 weights
+    w2 = view(2, 2048, 8, 18)
+    assert so.qg_gemm_w4a8_from_view(p(act), p(w2), p(out), None, None) == -1     # K mismatch
+
+
+def test_python_mirror_errors_match_reference():
+    import torch
+    import quant_gemm as q
+    with pytest.raises(RuntimeError, match="Input must be a CUDA tensor"):
+        q.quantize_q4_0(torch.zeros(4, 64))
+    with pytest.raises(RuntimeError, match="Weight must be a CUDA tensor"):
+        q.gemm_q4_0_q8_1(torch.zeros(4, 2, 18, dtype=torch.uint8), torch.zeros(1, 2, 36, dtype=torch.uint8), 4, 1, 64)
+    with pytest.raises(RuntimeError, match="K must be divisible by 32"):
+        q.gemm_q4_0_q8_1(torch.zeros(1, dtype=torch.uint8), torch.zeros(1, dtype=torch.uint8), 4, 1, 65)

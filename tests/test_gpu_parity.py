@@ -1,0 +1,227 @@
+"""GPU parity: the HIP kernels (through the C-ABI, via quant_gemm) vs the pinned CPU oracle.
+
+Bars:
+  * quantizer / dequantizer bytes: bit-exact;
+  * per-block int32 sumi: bit-exact, through the SAME decode path each kernel family uses;
+  * fp32 outputs: per-block terms are computed in the reference's operation order without
+    contraction, so the only admissible difference is fp32 summation order:
+    |C_gpu - C_ref| <= 2 * nb * 2^-24 * sum_b |term_b|   (oracle.summation_tol);
+  * vs FP32 (gemm_fp32_reference): NMSE <= 5e-3 for Q4_0 x Q8_1 on the step4 U[-1,1] recipe
+    (BASELINE.json north_star), per-format bounds for the all-quants config.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+WTYPES = [2, 3, 6, 7]
+ALGOS = {"gemv": 1, "generic": 3}
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def make_case(O, m, n, k, t, seed=42):
+    a, b = O.fill_uniform_step4(m, n, k, seed)
+    return a, b, O.quantize(a, O.Q8_1), O.quantize(b, t)
+
+
+def assert_close_to_oracle(O, c_gpu, aq, bq, t):
+    c_ref, s = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    tol = O.summation_tol(aq, bq, s, t)
+    err = np.abs(c_gpu.astype(np.float64) - c_ref)
+    assert (err <= tol).all(), f"max err {err.max()} vs tol {tol[err > tol].min()}"
+    return c_ref
+
+
+# ------------------------------------------------------------------------------- quantizers
+def edge_rows():
+    rng = np.random.default_rng(1)
+    rows = [np.zeros(64, np.float32),                                  # amax = 0 -> d = 0, id = 0
+            np.full(64, -3.0, np.float32),
+            (np.arange(64, dtype=np.float32) - 31.5) / 8.0,             # exact ties for Q4_0 / Q8_1
+            rng.standard_normal(64).astype(np.float32) * 1e-6,
+            rng.standard_normal(64).astype(np.float32) * 1e3,
+            np.where(np.arange(64) % 2 == 0, 1.0, -1.0).astype(np.float32)]
+    return np.stack(rows)
+
+
+@pytest.mark.parametrize("t,variant", [(9, 0), (9, 1), (2, 0), (8, 0), (3, 0), (6, 0), (7, 0)])
+def test_quantizer_bytes_bit_exact(O, qg, t, variant):
+    a, b = O.fill_uniform_step4(64, 64, 4096)
+    for x in (a, b, edge_rows()):
+        got = host(qg.quantize(dev(x), t, variant))
+        want = O.quantize(x, t, variant)
+        assert np.array_equal(got, want)
+
+
+def test_quantize_reference_names(O, qg):
+    a, b = O.fill_uniform_step4(3, 5, 1024)
+    assert np.array_equal(host(qg.quantize_q8_1(dev(a))), O.quantize(a, O.Q8_1))
+    assert np.array_equal(host(qg.quantize_q4_0(dev(b))), O.quantize(b, O.Q4_0))
+    x3 = b.reshape(5, 4, 256)  # leading dims preserved: [..., K] -> [..., K/32, 18]
+    assert host(qg.quantize_q4_0(dev(x3))).shape == (5, 4, 8, 18)
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8, 9])
+def test_dequantize_bit_exact(O, qg, t):
+    _, b = O.fill_uniform_step4(1, 16, 2048)
+    q = O.quantize(b, t)
+    assert np.array_equal(host(qg.dequantize(dev(q), t)), O.dequantize(q, t))
+    if t == 2:
+        assert np.array_equal(host(qg.dequantize_q4_0(dev(q), 2048)), O.dequantize(q, t))
+
+
+# ------------------------------------------------------------------------------- sumi (integer path)
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("algo", ["gemv", "generic"])
+@pytest.mark.parametrize("m,n,k", [(1, 64, 4096), (3, 37, 2048), (8, 16, 4096), (2, 5, 16384)])
+def test_sumi_bit_exact(O, qg, t, algo, m, n, k):
+    _, _, aq, bq = make_case(O, m, n, k, t)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t, ALGOS[algo]))
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+
+
+# ------------------------------------------------------------------------------- outputs
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("m", [1, 2, 3, 4, 5, 8])
+def test_gemv_matches_oracle(O, qg, t, m):
+    n, k = 300, 4096
+    _, _, aq, bq = make_case(O, m, n, k, t, seed=m)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=1))
+    assert_close_to_oracle(O, c, aq, bq, t)
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 32), (1, 3, 96), (2, 7, 288), (4, 65, 4128), (1, 4097, 256),
+                                   (9, 33, 512), (16, 64, 1024), (1, 5, 14336), (3, 17, 8192)])
+def test_auto_dispatch_shapes(O, qg, m, n, k):
+    """Ragged N, K not a multiple of 256, tiny and large K, M across the GEMV/prefill split."""
+    _, _, aq, bq = make_case(O, m, n, k, 2)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, 2))
+    assert_close_to_oracle(O, c, aq, bq, 2)
+
+
+def test_empty_is_noop(qg):
+    import torch
+    u8 = dict(dtype=torch.uint8, device="cuda")
+    assert qg.gemm_w4a8(torch.zeros(0, **u8), torch.zeros(8 * 2 * 18, **u8), 0, 8, 64).shape == (0, 8)
+    assert qg.gemm_w4a8(torch.zeros(2 * 36, **u8), torch.zeros(0, **u8), 1, 0, 64).shape == (1, 0)
+    assert qg.quantize_q8_1(torch.zeros((0, 64), device="cuda")).shape == (0, 2, 36)
+
+
+def test_misaligned_weights_take_generic_path(O, qg):
+    import torch
+    m, n, k = 1, 40, 1024
+    _, _, aq, bq = make_case(O, m, n, k, 2)
+    raw = torch.zeros(bq.size + 2, dtype=torch.uint8, device="cuda")
+    raw[2:] = dev(bq.ravel())
+    w = raw[2:]  # 2-byte aligned only: the 16-B GEMV loads are not legal
+    assert w.data_ptr() % 16 != 0
+    c = torch.empty((m, n), dtype=torch.float32, device="cuda")
+    lib = qg._lib.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.qg_gemm_w4a8_ex(ctypes.c_void_p(dev(aq).data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                               ctypes.c_void_p(c.data_ptr()), m, n, k, 2, 1, st) == -3  # GEMV refuses
+    a_t = dev(aq)
+    assert lib.qg_gemm_w4a8(ctypes.c_void_p(a_t.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                            ctypes.c_void_p(c.data_ptr()), m, n, k, 2, st) == 0
+    assert_close_to_oracle(O, host(c), aq, bq, 2)
+
+
+@pytest.mark.parametrize("t,sym", [(2, "gemm_q4_0_q8_1"), (3, "gemm_q4_1_q8_1"), (6, "gemm_q5_0_q8_1"),
+                                   (7, "gemm_q5_1_q8_1")])
+@pytest.mark.parametrize("ntok", [1, 2, 6])
+def test_weight_major_api(O, qg, t, sym, ntok):
+    """python/quant_gemm convention: out[M_w, N_tok] = W @ A^T (kernels/gemm/gemm_quant_formats.cuh:312)."""
+    mw, k = 130, 4096
+    _, _, aq, wq = make_case(O, ntok, mw, k, t)
+    out = host(getattr(qg, sym)(dev(wq), dev(aq), mw, ntok, k))
+    assert out.shape == (mw, ntok)
+    assert_close_to_oracle(O, np.ascontiguousarray(out.T), aq, wq, t)
+
+
+def test_reference_harness_convention(O, qg):
+    """python/test_operator.py:236-240: kernel(weight_q, activation_q, N, M, K).T == C[M, N]."""
+    m, n, k = 4, 96, 1024
+    a, b, aq, bq = make_case(O, m, n, k, 2)
+    out = host(qg.gemm_q4_0_q8_1(dev(bq), dev(aq), n, m, k)).T
+    assert_close_to_oracle(O, np.ascontiguousarray(out), aq, bq, 2)
+
+
+def test_ggml_view_adapter(O, qg):
+    import torch
+    m, n, k = 2, 48, 512
+    _, _, aq, bq = make_case(O, m, n, k, 2)
+    a_t, b_t = dev(aq), dev(bq)
+    c = torch.empty((m, n), dtype=torch.float32, device="cuda")
+
+    class View(ctypes.Structure):
+        _fields_ = [("data", ctypes.c_void_p), ("type", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
+                    ("nb", ctypes.c_size_t * 4)]
+
+    def view(ptr, t, ne0, ne1, row):
+        v = View()
+        v.data, v.type = ptr, t
+        v.ne[:] = [ne0, ne1, 1, 1]
+        v.nb[:] = [0, row, row * ne1, row * ne1]
+        return v
+
+    act = view(a_t.data_ptr(), 9, k, m, (k // 32) * 36)
+    w = view(b_t.data_ptr(), 2, k, n, (k // 32) * 18)
+    out = view(c.data_ptr(), 0, n, m, n * 4)
+    out.nb[0] = 4
+    lib = qg._lib.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.qg_gemm_w4a8_from_view(ctypes.byref(act), ctypes.byref(w), ctypes.byref(out), b"dp4a", st) == 0
+    assert_close_to_oracle(O, host(c), aq, bq, 2)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "w4a8_*.npz"))), ids=os.path.basename)
+def test_golden_vectors_on_gpu(O, qg, path):
+    """The reference's own Python definition outputs, reproduced by the HIP path."""
+    g = np.load(path)
+    m, n, k, t = (int(g[x]) for x in ("m", "n", "k", "wtype"))
+    c = host(qg.gemm_w4a8(dev(g["a_q"]), dev(g["b_q"]), m, n, k, t))
+    _, s = O.gemm_w4a8(g["a_q"], g["b_q"], t, want_sumi=True)
+    tol = O.summation_tol(g["a_q"], g["b_q"], s, t) + 1e-6 * np.abs(g["c_ref"])
+    assert (np.abs(c.astype(np.float64) - g["c_ref"]) <= tol).all()
+
+
+# ------------------------------------------------------------------------------- BASELINE configs, full size
+@pytest.mark.parametrize("m,n,k,bound", [(1, 4096, 4096, 5e-3), (32, 4096, 4096, 5e-3), (1, 32000, 4096, 5e-3)])
+def test_baseline_q4_0_full_size(O, qg, m, n, k, bound):
+    """BASELINE configs[1], [2], [4] at full size: oracle parity and NMSE vs FP32 <= 5e-3."""
+    a, b, aq, bq = make_case(O, m, n, k, 2)
+    # the device quantizers produce the same bytes the oracle does
+    aq_d = qg.quantize_q8_1(dev(a))
+    bq_d = qg.quantize_q4_0(dev(b))
+    assert np.array_equal(host(aq_d), aq) and np.array_equal(host(bq_d), bq)
+    c = host(qg.gemm_w4a8(aq_d, bq_d, m, n, k))
+    c_ref = assert_close_to_oracle(O, c, aq, bq, 2)
+    import torch
+    c_fp32 = host(torch.from_numpy(a).cuda().double() @ torch.from_numpy(b).cuda().double().T)
+    assert O.nmse(c, c_fp32) <= bound
+    assert abs(O.nmse(c, c_fp32) - O.nmse(c_ref, c_fp32)) < 1e-9
+
+
+@pytest.mark.parametrize("t,bound", [(2, 5e-3), (3, 4.5e-3), (6, 1.5e-3), (7, 1.2e-3)])
+def test_allquants_full_size(O, qg, t, bound):
+    """BASELINE configs[3]: Q4_1/Q5_0/Q5_1 (and Q4_0) x Q8_1 GEMV at M=1, N=K=4096."""
+    a, b, aq, bq = make_case(O, 1, 4096, 4096, t)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), 1, 4096, 4096, t))
+    assert_close_to_oracle(O, c, aq, bq, t)
+    assert O.nmse(c, O.gemm_fp32(a, b)) <= bound

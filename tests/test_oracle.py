@@ -1,0 +1,166 @@
+"""Pin the CPU oracle (oracle/qg_oracle.c) before trusting it as the parity checker.
+
+Every expected value here comes from the reference: its own recorded known answers, its
+self-contained KAT programs compiled from /root/reference into oracle/_ref/ (when present), and
+golden vectors produced by its runnable Python definitions (tests/golden/make_golden.py).
+"""
+import glob
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+REF_BIN = os.path.join(os.path.dirname(HERE), "oracle", "_ref")
+
+with open(os.path.join(GOLD, "kat.json")) as f:
+    KAT = json.load(f)
+
+
+def test_half_conversion_exhaustive(O):
+    # every fp16 bit pattern -> float matches numpy; float -> half RNE matches numpy on a sweep
+    L = O.lib()
+    bits = np.arange(0, 1 << 16, dtype=np.uint32)
+    ref = bits.astype(np.uint16).view(np.float16).astype(np.float32)
+    got = np.array([L.qgo_h2f(int(b)) for b in bits[::97]], np.float32)
+    r = ref[::97]
+    ok = (got == r) | (np.isnan(got) & np.isnan(r))
+    assert ok.all()
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.standard_normal(20000).astype(np.float32) * 10.0 ** rng.integers(-9, 6, 20000),
+                         np.float32([0.0, -0.0, 65504.0, 65520.0, 1e-8, 6.1e-5, 5.96e-8, 2.98e-8])]).astype(np.float32)
+    with np.errstate(over="ignore"):
+        want = xs.astype(np.float16).view(np.uint16)
+    got = np.array([L.qgo_f2h(float(x)) for x in xs], np.uint16)
+    assert (got == want).all()
+
+
+def test_kat3_dot4(O):
+    for a, b, want in KAT["kat3_dp4a"]["cases"]:
+        assert O.dot4(a, b) == want
+
+
+def test_kat1_step4_compensation(O):
+    k = KAT["kat1_step4_compensation"]
+    a = np.array(k["a"], np.float32)[None]
+    w = np.array(k["w"], np.float32)[None]
+    fp32 = O.gemm_fp32(a, w)[0, 0]
+    assert f"{fp32:.6f}" == k["fp32"]
+    aq = O.quantize(a, O.Q8_1)
+    wq = O.quantize(w, O.Q4_0)
+    assert wq[0, 0, :2].view(np.uint16)[0] == int(k["d_w_half"], 16)
+    assert aq[0, 0, :2].view(np.uint16)[0] == int(k["d_a_half"], 16)
+    assert aq[0, 0, 2:4].view(np.uint16)[0] == int(k["s_a_half"], 16)
+    assert wq[0, 0, 2:].tobytes().hex() == k["q4_qs"]
+    assert aq[0, 0, 4:].view(np.int8).tolist() == k["q8_qs"]
+    c, s = O.gemm_w4a8(aq, wq, O.Q4_0, want_sumi=True)
+    assert int(s[0, 0, 0]) == k["sumi"]
+    assert f"{c[0, 0]:.6f}" == k["with_compensation"]
+    assert f"{O.vec_dot_q4_0_q8_1(wq, aq):.6f}" == k["with_compensation"]
+    d_w = np.float32(np.float16(wq[0, 0, :2].view(np.float16)[0]))
+    d_a = np.float32(aq[0, 0, :2].view(np.float16)[0])
+    assert f"{np.float32(s[0, 0, 0]) * d_a * d_w:.6f}" == k["without_compensation"]
+
+
+def _kat2_inputs():
+    i = np.arange(32)
+    return ((i % 16) - 8).astype(np.float32)[None], (i - 16).astype(np.float32)[None]
+
+
+def test_kat2_cpu_ref_formula(O):
+    k = KAT["kat2_test_cpu_ref"]
+    w, a = _kat2_inputs()
+    assert f"{O.gemm_fp32(a, w)[0, 0]:.6f}" == k["reference"]
+    aq = O.quantize(a, O.Q8_1, variant=1)  # tests/framework to_q8_1: s = d * sum(q)
+    wq = O.quantize(w, O.Q4_0)
+    _, s = O.gemm_w4a8(aq, wq, O.Q4_0, want_sumi=True)
+    assert int(s[0, 0, 0]) == k["sumi"]
+    assert int(aq[0, 0, 4:].view(np.int8).astype(np.int32).sum()) == k["sum_a_q"]
+    assert f"{np.float32(aq[0, 0, 2:4].view(np.float16)[0]):.6f}" == k["s_a"]
+    # the KAT keeps fp32 (unrounded) scales: same block formula on those reproduces its output
+    d_w = np.float32(8.0) / np.float32(7.0)
+    d_a = np.float32(16.0) / np.float32(127.0)
+    s_a = np.float32(k["sum_a_q"]) * d_a
+    out = d_w * (d_a * np.float32(k["sumi"]) - np.float32(8.0) * s_a)
+    assert f"{out:.6f}" == k["result"]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_BIN, "test_cpu_ref")),
+                    reason="reference KAT binaries not built (reference tree absent)")
+def test_kat2_against_compiled_reference(O):
+    """Run the reference's own test_cpu_ref / test_dot / test_q8_1 and compare with the oracle."""
+    out = subprocess.run([os.path.join(REF_BIN, "test_cpu_ref")], capture_output=True, text=True, check=True).stdout
+    w, a = _kat2_inputs()
+    aq = O.quantize(a, O.Q8_1, variant=1)
+    wq = O.quantize(w, O.Q4_0)
+    _, s = O.gemm_w4a8(aq, wq, O.Q4_0, want_sumi=True)
+    assert f"sumi = {int(s[0, 0, 0])}" in out
+    qs0 = wq[0, 0, 2]
+    assert f"qs[0]=0x{qs0:02x}" in out
+    for i in range(4):
+        assert f"qs[{i}]={int(aq[0, 0, 4 + i].view(np.int8))} " in out
+    out2 = subprocess.run([os.path.join(REF_BIN, "test_dot")], capture_output=True, text=True, check=True).stdout
+    assert f"sumi = {int(s[0, 0, 0])}" in out2
+    out3 = subprocess.run([os.path.join(REF_BIN, "test_q8_1")], capture_output=True, text=True, check=True).stdout
+    x = ((np.arange(32) - 16) * np.float32(0.1)).astype(np.float32)[None]
+    q = O.quantize(x, O.Q8_1, variant=1)
+    assert f"sum_q = {int(q[0, 0, 4:].view(np.int8).astype(np.int32).sum())}" in out3
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "w4a8_*.npz"))), ids=os.path.basename)
+def test_golden_w4a8(O, path):
+    """Oracle == the reference's Python definition on the same bytes (it sums in fp64, so allow
+    fp32-summation-level differences), and the inputs regenerate bit-exactly."""
+    g = np.load(path)
+    m, n, k, t, seed = (int(g[x]) for x in ("m", "n", "k", "wtype", "seed"))
+    a, b = O.fill_uniform_step4(m, n, k, seed)
+    assert np.array_equal(a[0, :8], g["a_head"]) and np.array_equal(b[0, :8], g["b_head"])
+    aq = O.quantize(a, O.Q8_1)
+    bq = O.quantize(b, t)
+    assert np.array_equal(aq, g["a_q"]) and np.array_equal(bq, g["b_q"])
+    c, s = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    tol = O.summation_tol(aq, bq, s, t) + 1e-6 * np.abs(g["c_ref"])
+    assert (np.abs(c.astype(np.float64) - g["c_ref"]) <= tol).all()
+    assert np.array_equal(O.gemm_fp32(a, b), g["c_fp32"])
+
+
+def test_golden_plumbing_nmse(O):
+    """BASELINE configs[0]: W4A8 vs FP32 NMSE equals the reference's recorded 4.2747e-3."""
+    g = np.load(os.path.join(GOLD, "w4a8_q4_0_plumbing.npz"))
+    c = O.gemm_w4a8(g["a_q"], g["b_q"], O.Q4_0)
+    assert f"{O.nmse(c, g['c_fp32']):.4e}" == f"{KAT['nmse_vs_fp32']['m1_n128_k256']:.4e}"
+
+
+def test_golden_quantize_q8_1(O):
+    """Oracle Q8_1 bytes vs the reference definition's quantizer. The definition uses x/d and
+    np.round (ties to even) where include/quantize.h uses x*(1/d) and roundf; the two can only
+    differ by one code on elements whose scaled value is within an ulp of a .5 tie."""
+    g = np.load(os.path.join(GOLD, "quantize_q8_1_m16k128.npz"))
+    q = O.quantize(g["x"], O.Q8_1)
+    ref = g["q_ref"]
+    assert np.array_equal(q[..., :4], ref[..., :4])  # d and s halves identical
+    diff = q[..., 4:].view(np.int8).astype(int) - ref[..., 4:].view(np.int8).astype(int)
+    assert np.abs(diff).max() <= 1
+    x = g["x"].reshape(16, 4, 32)
+    d = np.abs(x).max(-1, keepdims=True) / np.float32(127.0)
+    frac = np.abs((x * (np.float32(1.0) / d)) % 1.0 - 0.5)
+    assert (frac[diff != 0] < 1e-4).all()
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7])
+def test_allquants_nmse_small(O, t):
+    """All-quants formulas (no /4) stay within the FP32-anchored bounds at a CPU-fast size."""
+    a, b = O.fill_uniform_step4(2, 256, 1024)
+    c = O.gemm_w4a8(O.quantize(a, O.Q8_1), O.quantize(b, t), t)
+    bound = {2: 8e-3, 3: 8e-3, 6: 3e-3, 7: 3e-3}[t]
+    assert O.nmse(c, O.gemm_fp32(a, b)) < bound
+
+
+def test_dequantize_roundtrip(O):
+    a, b = O.fill_uniform_step4(4, 4, 256)
+    for t in (2, 3, 6, 7, 8, 9):
+        x = O.dequantize(O.quantize(b, t), t)
+        assert np.abs(x - b).max() < {2: 0.08, 3: 0.075, 6: 0.04, 7: 0.04, 8: 0.005, 9: 0.005}[t]
