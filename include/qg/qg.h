@@ -66,6 +66,12 @@ int qg_gemm_w4a8(const void* A_q8_1, const void* B, float* C, int M, int N, int 
 int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, int algo,
                     qg_stream_t stream);
 
+/* Strided batch of independent products (e.g. the experts of an MoE layer, or several projections
+ * sharing nothing): item i uses A + i*strideA, B + i*strideB (bytes) and C + i*strideC (floats).
+ * One launch on the GEMV path (M <= 8), so the per-launch cost is paid once for the batch. */
+int qg_gemm_w4a8_strided_batched(const void* A_q8_1, int64_t strideA, const void* B, int64_t strideB, float* C,
+                                 int64_t strideC, int batch, int M, int N, int K, int wtype, qg_stream_t stream);
+
 /* ---- weight-major twins (kernels/gemm/gemm_quant_formats.cuh:343-428) ---------------------
  * out[M][N] = W[M][K/32] . A[N][K/32]^T, M = weight rows, N = tokens. */
 int qg_gemm_q4_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);

@@ -33,18 +33,41 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     if (g.M == 0 || g.N == 0) return QG_OK;
     if (!g.A || !g.B || (!g.C && !g.sumi)) return QG_ERR_INVALID_ARG;
     if (((uintptr_t)g.B & 1) != 0) return QG_ERR_ALIGN;  // fp16 fields: 2-byte alignment is the floor
+    if (g.batch < 0) return QG_ERR_INVALID_ARG;
+    if (g.batch == 0) return QG_OK;
+    if (g.batch > 1 && (((uintptr_t)g.sB & 1) != 0 || (g.sA & 3) != 0)) return QG_ERR_ALIGN;
     if (algo == QG_ALGO_AUTO) algo = select_algo(g);
-    switch (algo) {
-        case QG_ALGO_GEMV:
-            if (!gemv_eligible(g)) return QG_ERR_UNSUPPORTED;
+    if (algo == QG_ALGO_GEMV) {
+        if (!gemv_eligible(g) || (g.batch > 1 && (g.sB % 16 != 0))) {
+            if (g.batch == 1) return QG_ERR_UNSUPPORTED;
+            algo = QG_ALGO_GENERIC;  // batch strides break the vector-load alignment: per-item path
+        } else {
+            if (g.batch > 65535) return QG_ERR_INVALID_ARG;
             return hip_status(launch_gemv(g, st));
-        case QG_ALGO_MFMA:
-            if (!mfma_eligible(g)) return QG_ERR_UNSUPPORTED;
-            return hip_status(launch_mfma(g, st));
-        case QG_ALGO_GENERIC:
-            return hip_status(launch_generic(g, st));
+        }
     }
-    return QG_ERR_INVALID_ARG;
+    // MFMA and generic kernels take one product per launch: enqueue the batch item by item.
+    for (int i = 0; i < g.batch; ++i) {
+        GemmArgs gi = g;
+        gi.batch = 1;
+        gi.A = (const uint8_t*)g.A + (long)i * g.sA;
+        gi.B = (const uint8_t*)g.B + (long)i * g.sB;
+        if (g.C) gi.C = g.C + (long)i * g.sC;
+        int rc;
+        switch (algo) {
+            case QG_ALGO_MFMA:
+                if (!mfma_eligible(gi)) return QG_ERR_UNSUPPORTED;
+                rc = hip_status(launch_mfma(gi, st));
+                break;
+            case QG_ALGO_GENERIC:
+                rc = hip_status(launch_generic(gi, st));
+                break;
+            default:
+                return QG_ERR_INVALID_ARG;
+        }
+        if (rc != QG_OK) return rc;
+    }
+    return QG_OK;
 }
 
 int block_bytes(int t) {
@@ -77,6 +100,15 @@ int qg_gemm_w4a8_ex(const void* A, const void* B, float* C, int M, int N, int K,
     g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
     g.ldc_m = N; g.ldc_n = 1;
     return run_gemm(g, algo, (hipStream_t)stream);
+}
+
+int qg_gemm_w4a8_strided_batched(const void* A, int64_t strideA, const void* B, int64_t strideB, float* C,
+                                 int64_t strideC, int batch, int M, int N, int K, int wtype, qg_stream_t stream) {
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.batch = batch; g.sA = strideA; g.sB = strideB; g.sC = strideC;
+    return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)stream);
 }
 
 int qg_gemm_w4a8(const void* A, const void* B, float* C, int M, int N, int K, int wtype, qg_stream_t stream) {

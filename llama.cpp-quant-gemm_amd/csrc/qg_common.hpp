@@ -64,6 +64,14 @@ template <int OFF> __device__ __forceinline__ uint32_t ld16(const uint32_t* w) {
     else return w[OFF / 4] >> 16;
 }
 
+// c ? a : b on VALUES. Both operands are pinned in VGPRs first: a plain ternary over two elements
+// of a register-resident array gets folded into a load through a selected pointer, which demotes
+// the whole array to scratch memory.
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
+    asm volatile("" : "+v"(a), "+v"(b));
+    return c ? a : b;
+}
+
 // Spread 4 bits (x in [0,15]) to bit 4 of each byte: bit k -> bit 8k+4. v_mul_u32_u24 is full rate.
 __device__ __forceinline__ uint32_t spread4_bit4(uint32_t x) {
     return ((uint32_t)__umul24(x, 0x00204081u) & 0x01010101u) << 4;

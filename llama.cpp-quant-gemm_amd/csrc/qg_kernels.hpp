@@ -15,7 +15,8 @@ struct GemmArgs {
     int M = 0, N = 0, K = 0;
     int wtype = 0;
     long ldc_m = 0, ldc_n = 1;
-    bool nontemporal = true;     // weight stream loads with the nt hint
+    int batch = 1;               // strided batch of independent products (GEMV path)
+    long sA = 0, sB = 0, sC = 0; // batch strides: bytes, bytes, floats
 };
 
 // GEMV / small batch (M <= 8), register-resident super-block decode + v_dot4.

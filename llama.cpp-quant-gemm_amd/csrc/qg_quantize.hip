@@ -15,6 +15,10 @@
 namespace qg {
 
 __device__ __forceinline__ uint32_t f2h_bits(float f) {
+    // Materialise the fp32 value first: without this barrier the compiler folds a preceding fmul
+    // into a mixed-precision v_fma_mix (one rounding straight to f16), which differs from the
+    // reference's double rounding (f32 product, then __float2half RNE) at f16 ties.
+    asm volatile("" : "+v"(f));
     return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);  // RNE, as __float2half
 }
 

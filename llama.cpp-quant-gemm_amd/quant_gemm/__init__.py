@@ -131,6 +131,28 @@ def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int
     return out
 
 
+def gemm_w4a8_batched(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
+                      wtype: int = Q4_0) -> torch.Tensor:
+    """Strided batch of independent activation-major products: activation_q [B, M, K/32, 36],
+    weight_q [B, N, K/32, bb] -> C [B, M, N]. One launch on the GEMV path (M <= 8)."""
+    _require(activation_q.is_cuda and weight_q.is_cuda, "Inputs must be CUDA tensors")
+    _require(activation_q.dtype == torch.uint8 and weight_q.dtype == torch.uint8, "Inputs must be uint8")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    B = weight_q.shape[0]
+    bb = BLOCK_BYTES[wtype]
+    _require(activation_q.shape[0] == B, "batch mismatch")
+    _require(activation_q[0].numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    _require(weight_q[0].numel() == N * (K // 32) * bb, "Weight shape mismatch")
+    a = activation_q.contiguous()
+    w = weight_q.contiguous()
+    out = torch.empty((B, M, N), dtype=torch.float32, device=w.device)
+    with torch.cuda.device(w.device):
+        _lib.check(_lib.load().qg_gemm_w4a8_strided_batched(
+            _ptr(a), a[0].numel(), _ptr(w), w[0].numel(), _ptr(out), M * N, B, M, N, K, wtype,
+            _stream(w.device)), "gemm_w4a8_batched")
+    return out
+
+
 def _gemm_weight_major(sym: str, wtype: int, weight_q, activation_q, M, N, K):
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
     _check_blocks(weight_q, "Weight", M, K, BLOCK_BYTES[wtype])
@@ -189,6 +211,6 @@ __all__ = [
     "quantize_q4_0", "quantize_q8_1", "gemm_q4_0_q8_1", "dequantize_q4_0",
     "QK4_0", "QK8_1", "BLOCK_Q4_0_BYTES", "BLOCK_Q8_1_BYTES",
     "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
-    "debug_sumi", "select_algo", "version",
+    "gemm_w4a8_batched", "debug_sumi", "select_algo", "version",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

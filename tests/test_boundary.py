@@ -62,7 +62,9 @@ def test_static_queries(lib):
     assert [so.qg_block_bytes(t) for t in (2, 3, 6, 7, 8, 9, 0)] == [18, 20, 22, 24, 34, 36, 0]
     assert so.qg_select_algo(1, 4096, 4096, 2) == 1      # decode -> GEMV
     assert so.qg_select_algo(8, 4096, 4096, 6) == 1
-    assert so.qg_select_algo(1, 4096, 4128, 2) == 3      # K % 256 != 0 -> generic
+    assert so.qg_select_algo(32, 4096, 4096, 2) == 2     # prefill -> MFMA
+    assert so.qg_select_algo(1, 4096, 4128, 2) == 3      # K/32 odd -> generic
+    assert so.qg_select_algo(16, 64, 4128, 7) == 3
     assert so.qg_select_algo(1, 4096, 33, 2) == -1
     assert so.qg_status_string(-2).decode().startswith("K must be")
 

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 WTYPES = [2, 3, 6, 7]
-ALGOS = {"gemv": 1, "generic": 3}
+ALGOS = {"gemv": 1, "mfma": 2, "generic": 3}
 
 
 def dev(x):
@@ -56,6 +56,13 @@ def edge_rows():
             rng.standard_normal(64).astype(np.float32) * 1e-6,
             rng.standard_normal(64).astype(np.float32) * 1e3,
             np.where(np.arange(64) % 2 == 0, 1.0, -1.0).astype(np.float32)]
+    # s = sum(x) lands exactly on an f16 tie after fp32 rounding (1 + 2^-11) while the exact sum
+    # is just above it: catches a fused add->f16 conversion (single rounding) in the quantizer
+    tie = np.zeros(64, np.float32)
+    tie[0] = 1.0
+    tie[31] = np.float32(2.0 ** -11 + 2.0 ** -30)
+    tie[32:] = np.linspace(-0.7, 0.9, 32, dtype=np.float32)
+    rows.append(tie)
     return np.stack(rows)
 
 
@@ -87,9 +94,11 @@ def test_dequantize_bit_exact(O, qg, t):
 
 # ------------------------------------------------------------------------------- sumi (integer path)
 @pytest.mark.parametrize("t", WTYPES)
-@pytest.mark.parametrize("algo", ["gemv", "generic"])
-@pytest.mark.parametrize("m,n,k", [(1, 64, 4096), (3, 37, 2048), (8, 16, 4096), (2, 5, 16384)])
+@pytest.mark.parametrize("algo", ["gemv", "mfma", "generic"])
+@pytest.mark.parametrize("m,n,k", [(1, 64, 4096), (3, 37, 2048), (8, 16, 4096), (2, 5, 16384), (40, 70, 1024)])
 def test_sumi_bit_exact(O, qg, t, algo, m, n, k):
+    if algo == "gemv" and m > 8:
+        pytest.skip("GEMV path is M <= 8")
     _, _, aq, bq = make_case(O, m, n, k, t)
     got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t, ALGOS[algo]))
     _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
@@ -104,6 +113,35 @@ def test_gemv_matches_oracle(O, qg, t, m):
     _, _, aq, bq = make_case(O, m, n, k, t, seed=m)
     c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=1))
     assert_close_to_oracle(O, c, aq, bq, t)
+
+
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("m", [9, 16, 32, 33, 100])
+def test_mfma_matches_oracle(O, qg, t, m):
+    n, k = 96, 2048
+    _, _, aq, bq = make_case(O, m, n, k, t, seed=m)
+    assert qg.select_algo(m, n, k, t) == 2
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=2))
+    assert_close_to_oracle(O, c, aq, bq, t)
+
+
+@pytest.mark.parametrize("m,n,k", [(12, 33, 512), (64, 4096, 256), (32, 65, 8192)])
+def test_mfma_ragged(O, qg, m, n, k):
+    _, _, aq, bq = make_case(O, m, n, k, 2)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, 2, algo=2))
+    assert_close_to_oracle(O, c, aq, bq, 2)
+
+
+@pytest.mark.parametrize("m,t", [(1, 2), (3, 6), (12, 2)])
+def test_strided_batched(O, qg, m, t):
+    """One launch over independent products (GEMV path) == per-item oracle results."""
+    nbatch, n, k = 5, 130, 1024
+    items = [make_case(O, m, n, k, t, seed=100 + i) for i in range(nbatch)]
+    a = np.stack([it[2] for it in items])
+    b = np.stack([it[3] for it in items])
+    out = host(qg.gemm_w4a8_batched(dev(a), dev(b), m, n, k, t))
+    for i in range(nbatch):
+        assert_close_to_oracle(O, out[i], a[i], b[i], t)
 
 
 @pytest.mark.parametrize("m,n,k", [(1, 1, 32), (1, 3, 96), (2, 7, 288), (4, 65, 4128), (1, 4097, 256),
