@@ -36,4 +36,10 @@ fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
 fi
+if [[ "$STEPS" == all || "$STEPS" == *pmc* ]]; then
+  # PMC counters in their own passes (kernel trace only beside them), FETCH_SIZE and WRITE_SIZE
+  # separately (MI355X_MICROARCH.md: they cannot share a TCC pass)
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+fi
 echo done

@@ -1,0 +1,89 @@
+// test_capi.cpp — C++ host-side driver over the C-ABI (include/qg/qg.hpp), in the shape of the
+// reference's tests/step4_w4a8_gemm.cu: glibc srand(42) U[-1,1] inputs (A then B), quantize on the
+// GPU, run the W4A8 GEMM through the reference-named wrappers, compare with the CPU oracle
+// (oracle/_build/libqg_oracle.so — this is a test; the product library never links the oracle).
+// Exit status 0 = parity held. Built and run by tests/test_cpp_driver.py on the GPU box.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "qg/qg.hpp"
+
+extern "C" {
+void qgo_fill_uniform_step4(unsigned seed, float* a, int64_t na, float* b, int64_t nb);
+void qgo_quantize_row_q8_1(const float* src, void* dst, int64_t k);
+void qgo_quantize_row_q4_0(const float* src, void* dst, int64_t k);
+void qgo_gemm_w4a8(const void* A, const void* B, float* C, int32_t* sumi, int M, int N, int K, int t);
+void qgo_gemm_fp32(const float* A, const float* B, float* C, int M, int N, int K);
+}
+
+#define HCK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "HIP %s @%d\n", hipGetErrorString(e_), __LINE__); return 2; } } while (0)
+
+static int run(int M, int N, int K) {
+    const int nb = K / 32;
+    std::vector<float> a((size_t)M * K), b((size_t)N * K), c_ref((size_t)M * N), c_fp32((size_t)M * N), c((size_t)M * N);
+    std::vector<qg_block_q8_1> aq((size_t)M * nb), aq_gpu((size_t)M * nb);
+    std::vector<qg_block_q4_0> bq((size_t)N * nb), bq_gpu((size_t)N * nb);
+    qgo_fill_uniform_step4(42, a.data(), a.size(), b.data(), b.size());
+    for (int r = 0; r < M; ++r) qgo_quantize_row_q8_1(&a[(size_t)r * K], &aq[(size_t)r * nb], K);
+    for (int r = 0; r < N; ++r) qgo_quantize_row_q4_0(&b[(size_t)r * K], &bq[(size_t)r * nb], K);
+    qgo_gemm_w4a8(aq.data(), bq.data(), c_ref.data(), nullptr, M, N, K, QG_TYPE_Q4_0);
+    qgo_gemm_fp32(a.data(), b.data(), c_fp32.data(), M, N, K);
+
+    float *da, *db, *dc, *dc2;
+    qg_block_q8_1* dA;
+    qg_block_q4_0* dB;
+    HCK(hipMalloc(&da, a.size() * 4));
+    HCK(hipMalloc(&db, b.size() * 4));
+    HCK(hipMalloc(&dc, c.size() * 4));
+    HCK(hipMalloc(&dc2, c.size() * 4));
+    HCK(hipMalloc(&dA, aq.size() * sizeof(qg_block_q8_1)));
+    HCK(hipMalloc(&dB, bq.size() * sizeof(qg_block_q4_0)));
+    HCK(hipMemcpy(da, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+    HCK(hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice));
+    hipStream_t st;
+    HCK(hipStreamCreate(&st));
+    qg_stream_t s = reinterpret_cast<qg_stream_t>(st);
+    qg::check(qg::quantize_q8_1_cuda(da, dA, (int64_t)a.size(), s), "quantize_q8_1");
+    qg::check(qg::quantize_q4_0_cuda(db, dB, (int64_t)b.size(), s), "quantize_q4_0");
+    qg::check(qg::gemm_w4a8_naive(dA, dB, dc, M, N, K, s), "gemm_w4a8_naive");          // activation-major
+    qg::check(qg::gemm_q4_0_q8_1(dB, dA, dc2, N, M, K, s), "gemm_q4_0_q8_1");          // weight-major [N][M]
+    HCK(hipStreamSynchronize(st));
+    HCK(hipMemcpy(aq_gpu.data(), dA, aq.size() * sizeof(qg_block_q8_1), hipMemcpyDeviceToHost));
+    HCK(hipMemcpy(bq_gpu.data(), dB, bq.size() * sizeof(qg_block_q4_0), hipMemcpyDeviceToHost));
+    HCK(hipMemcpy(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<float> c2(c.size());
+    HCK(hipMemcpy(c2.data(), dc2, c.size() * 4, hipMemcpyDeviceToHost));
+    if (memcmp(aq.data(), aq_gpu.data(), aq.size() * sizeof(qg_block_q8_1)) ||
+        memcmp(bq.data(), bq_gpu.data(), bq.size() * sizeof(qg_block_q4_0))) {
+        fprintf(stderr, "quantized bytes differ from the oracle\n");
+        return 1;
+    }
+    double e2 = 0, r2 = 0, maxrel = 0;
+    for (int m = 0; m < M; ++m)
+        for (int n = 0; n < N; ++n) {
+            const double ref = c_ref[(size_t)m * N + n], got = c[(size_t)m * N + n], got2 = c2[(size_t)n * M + m];
+            maxrel = fmax(maxrel, fabs(got - ref) / (1e-3 + fabs(ref)));
+            maxrel = fmax(maxrel, fabs(got2 - ref) / (1e-3 + fabs(ref)));
+            const double f = c_fp32[(size_t)m * N + n];
+            e2 += (got - f) * (got - f);
+            r2 += f * f;
+        }
+    printf("M=%d N=%d K=%d  max rel diff vs oracle %.3e  NMSE vs FP32 %.4e  (%s)\n", M, N, K, maxrel, e2 / r2,
+           qg_version());
+    hipFree(da); hipFree(db); hipFree(dc); hipFree(dc2); hipFree(dA); hipFree(dB);
+    hipStreamDestroy(st);
+    return (maxrel < 1e-4 && e2 / r2 < 5e-3) ? 0 : 1;
+}
+
+int main() {
+    int rc = 0;
+    rc |= run(1, 128, 256);     // BASELINE configs[0] plumbing shape
+    rc |= run(1, 4096, 4096);   // configs[1]
+    rc |= run(32, 512, 4096);   // prefill shape (MFMA path)
+    return rc;
+}

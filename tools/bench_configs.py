@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Measure every BASELINE.json config on one MI355X (secondary numbers for DESIGN.md §6).
+
+For each config: weights quantized on-GPU, rotated over enough resident copies to exceed the
+256 MB Infinity Cache, G back-to-back launches captured in a hipGraph, timed with HIP events on
+the launch stream; plus (GEMV path) the same G products as one strided-batched launch.
+Prints one JSON object per config and writes them to --out.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "llama.cpp-quant-gemm_amd"))
+
+import torch  # noqa: E402
+
+import quant_gemm as qg  # noqa: E402
+
+PEAK = 8000.0
+CONFIGS = [
+    ("q4_0", 1, 4096, 4096), ("q4_1", 1, 4096, 4096), ("q5_0", 1, 4096, 4096), ("q5_1", 1, 4096, 4096),
+    ("q4_0", 32, 4096, 4096), ("q4_0", 1, 32000, 4096), ("q4_0", 1, 4000, 4096),
+    ("q4_0", 8, 4096, 4096), ("q4_0", 1, 4096, 14336), ("q4_0", 2, 4096, 14336), ("q4_0", 512, 4096, 4096),
+]
+WT = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
+
+
+def measure(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
+    dev = torch.device("cuda", 0)
+    wt = WT[wname]
+    bb = qg.BLOCK_BYTES[wt]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    a = torch.rand((M, K), generator=gen, device=dev) * 2 - 1
+    b = torch.rand((N, K), generator=gen, device=dev) * 2 - 1
+    aq, bq = qg.quantize_q8_1(a), qg.quantize(b, wt)
+    c = qg.gemm_w4a8(aq, bq, M, N, K, wt)
+    ref = a.double() @ b.double().T
+    nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
+    del b, ref
+    wbytes = bq.numel()
+    R = max(2, math.ceil(600e6 / wbytes))
+    G = min(G, R)
+    copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
+    copies.copy_(bq.unsqueeze(0).expand_as(copies))
+    out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+    lib = qg._lib.load()
+    algo = lib.qg_select_algo(M, N, K, wt)
+
+    def step(stream):
+        for j in range(G):
+            st = lib.qg_gemm_w4a8(ctypes.c_void_p(aq.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                  ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt, stream)
+            assert st == 0, st
+
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        step(ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    for _ in range(2):
+        g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * G)
+    nbk = K // 32
+    byts = N * nbk * bb + M * nbk * 36 + M * N * 4
+    flops = 2.0 * M * N * K
+    res = {"wtype": wname, "M": M, "N": N, "K": K, "algo": {1: "gemv", 2: "mfma", 3: "generic"}.get(algo, algo),
+           "us_per_launch": round(us, 3), "gbps": round(byts / us / 1e3, 1), "frac_hbm": round(byts / us / 1e3 / PEAK, 4),
+           "tflops": round(flops / us / 1e6, 3), "nmse_vs_fp32": nmse, "algorithmic_bytes": byts, "launches": G}
+    if algo == 1:
+        bout = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+        cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        call = lambda: lib.qg_gemm_w4a8_strided_batched(  # noqa: E731
+            ctypes.c_void_p(aq.data_ptr()), 0, ctypes.c_void_p(copies.data_ptr()), wbytes,
+            ctypes.c_void_p(bout.data_ptr()), M * N, G, M, N, K, wt, cs)
+        for _ in range(2):
+            assert call() == 0
+        e0.record()
+        for _ in range(reps):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        ub = e0.elapsed_time(e1) * 1e3 / (reps * G)
+        res["batched"] = {"us_per_gemv": round(ub, 3), "gbps": round(byts / ub / 1e3, 1),
+                          "frac_hbm": round(byts / ub / 1e3 / PEAK, 4), "tflops": round(flops / ub / 1e6, 3)}
+        assert torch.equal(bout[0], out[0])
+    return res
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--gemvs", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    rows = []
+    for w, m, n, k in CONFIGS:
+        r = measure(w, m, n, k, args.gemvs, args.reps)
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+        torch.cuda.empty_cache()
+    if args.out:
+        json.dump(rows, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

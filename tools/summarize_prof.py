@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output for the qg kernels (kernel trace and/or PMC counters).
+
+    python tools/summarize_prof.py <rocprof_dir> [--pmc-json out.json] > summary.md
+
+Kernel-trace rows are grouped by (kernel, grid) so single-GEMV launches and strided-batched
+launches of the same kernel are reported separately. PMC rows (counter_collection.csv) are
+averaged per (kernel, grid); FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (on gfx950 it
+reads half the bytes of a wide coalesced stream) and reported as HBM bytes per launch.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import statistics as st
+
+
+def short(name: str) -> str:
+    name = name.split("(")[0]
+    return re.sub(r"^void ", "", name)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("d")
+    ap.add_argument("--pmc-json")
+    ap.add_argument("--key", default="q4_0_m1_n4096_k4096")
+    args = ap.parse_args()
+    out = []
+    for f in sorted(glob.glob(os.path.join(args.d, "**", "*kernel_trace.csv"), recursive=True)):
+        groups = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if "qg::" not in r["Kernel_Name"]:
+                continue
+            k = (short(r["Kernel_Name"]), r["Grid_Size_X"], r["Grid_Size_Y"], r["Workgroup_Size_X"], r["VGPR_Count"])
+            groups[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        out.append(f"### kernel trace: {os.path.relpath(f, args.d)}\n")
+        out.append("| kernel | grid x,y | WG | VGPR | calls | mean us | median us | min us | max us |")
+        out.append("|---|---|---|---|---|---|---|---|---|")
+        for (n, gx, gy, wg, vg), v in sorted(groups.items(), key=lambda kv: -len(kv[1])):
+            out.append(f"| `{n}` | {gx},{gy} | {wg} | {vg} | {len(v)} | {st.mean(v):.3f} | {st.median(v):.3f} | "
+                       f"{min(v):.3f} | {max(v):.3f} |")
+        out.append("")
+    pmc = {}
+    for f in sorted(glob.glob(os.path.join(args.d, "**", "*counter_collection.csv"), recursive=True)):
+        groups = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(f)):
+            if "qg::" not in r["Kernel_Name"]:
+                continue
+            k = (short(r["Kernel_Name"]), r.get("Grid_Size_X", r.get("Grid_Size", "")), r.get("Grid_Size_Y", ""))
+            groups[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        out.append(f"### counters: {os.path.relpath(f, args.d)}\n")
+        out.append("| kernel | grid x,y | counter | dispatches | mean | derived |")
+        out.append("|---|---|---|---|---|---|")
+        for (n, gx, gy), cs in groups.items():
+            for c, v in cs.items():
+                derived = ""
+                if c == "FETCH_SIZE":
+                    hbm = 2 * st.mean(v) * 1024
+                    derived = f"HBM read ≈ 2 x FETCH_SIZE x 1024 = {hbm:.0f} B/launch"
+                    pmc.setdefault(f"{n}|{gx},{gy}", {})["hbm_read_bytes_per_launch"] = hbm
+                if c == "WRITE_SIZE":
+                    pmc.setdefault(f"{n}|{gx},{gy}", {})["hbm_write_bytes_per_launch"] = st.mean(v) * 1024
+                out.append(f"| `{n}` | {gx},{gy} | {c} | {len(v)} | {st.mean(v):.1f} | {derived} |")
+        out.append("")
+    print("\n".join(out))
+    if args.pmc_json and pmc:
+        json.dump(pmc, open(args.pmc_json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
