@@ -44,7 +44,10 @@ template <int F, int BPL> struct gemv_geom {
 
 // ABL (tuning ablations, tools/gemv_probe.hip only; the product uses 0): 1 = skip the activation
 // staging (LDS left uninitialised), 2 = skip decode/dot (fold the weight words), 3 = both.
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool NT, bool SUMI, int ABL = 0>
+// DMA: the workgroup's weight rows (one contiguous span) are copied HBM -> LDS with
+// global_load_lds_dwordx4 (perfectly coalesced 1 KB per wave-instruction, no VGPRs), then each lane
+// reads its units from LDS; otherwise lanes load their units straight into VGPRs.
+template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool NT, bool SUMI, int ABL = 0, bool DMA = false>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                    int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
@@ -85,8 +88,31 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
             else dst[v] = p[v];
         }
     };
+    // DMA: weight span of this workgroup at the front of LDS, activation records after it
+    const int row0 = blockIdx.x * RPB;
+    const long row_bytes = (long)U * G::UB;
+    uint8_t* wlds = reinterpret_cast<uint8_t*>(lds);
+    uint32_t* alds = lds;
+    if constexpr (DMA) {
+        const long span = (long)max(0, min(RPB, N - row0)) * row_bytes;
+        alds = lds + (RPB * row_bytes + 15) / 16 * 4;
+        const uint8_t* src = B + (long)row0 * row_bytes;
+        const int nchunks = (int)((span + 1023) / 1024);
+        for (int j = tid >> 6; j < nchunks; j += WGS / 64) {
+            const long off = (long)j * 1024 + lane * 16;
+            if (off < span)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off),
+                                                 (__attribute__((address_space(3))) void*)(wlds + (long)j * 1024),
+                                                 16, 0, 0);
+        }
+    }
+    auto lds_unit = [&](LT (&dst)[G::NL], int u) {
+        const LT* p = reinterpret_cast<const LT*>(wlds + (long)(row - row0) * row_bytes + (long)(u < U ? u : 0) * G::UB);
+#pragma unroll
+        for (int v = 0; v < G::NL; ++v) dst[v] = p[v];
+    };
     LT cur[G::NL];
-    load_unit(cur, lir);
+    if constexpr (!DMA) load_unit(cur, lir);
 
     // 3) activations -> LDS records (the first NSTAGE*WGS dwords were loaded above; a K too
     //    large for that chunk stages the remainder here, after the weight stream is in flight)
@@ -98,10 +124,10 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
         const int u = b / BPL;
         const int rec = (m * U + u) * G::REC_DW + (b - u * BPL) * 12;
         if (w == 0) {
-            lds[rec + 8] = __float_as_uint(h2f(v & 0xFFFFu));
-            lds[rec + 9] = __float_as_uint(h2f(v >> 16));
+            alds[rec + 8] = __float_as_uint(h2f(v & 0xFFFFu));
+            alds[rec + 9] = __float_as_uint(h2f(v >> 16));
         } else {
-            lds[rec + w - 1] = v;
+            alds[rec + w - 1] = v;
         }
     };
 #pragma unroll
@@ -110,7 +136,11 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
         if (g < tot) stage(g, av[i]);
     }
     for (int g = tid + NSTAGE * WGS; g < tot; g += WGS) stage(g, A[g]);
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA is not tracked
     __syncthreads();
+    if constexpr (DMA) {
+        if (row_ok) lds_unit(cur, lir);
+    }
 
     float acc[MT];
 #pragma unroll
@@ -120,7 +150,13 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
     for (int j = 0; j < iters; ++j) {
         const int u = lir + j * LPR;
         LT nxt[G::NL];
-        if (j + 1 < iters) load_unit(nxt, u + LPR);
+        if (j + 1 < iters) {
+            if constexpr (DMA) {
+                if (row_ok) lds_unit(nxt, u + LPR);
+            } else {
+                load_unit(nxt, u + LPR);
+            }
+        }
         if constexpr ((ABL & 2) != 0) {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(cur);
             uint32_t x = 0;
@@ -135,7 +171,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     if (m < M) {
-                        const uint32_t* rec = lds + (m * U + u) * G::REC_DW + bi * 12;
+                        const uint32_t* rec = alds + (m * U + u) * G::REC_DW + bi * 12;
                         const uint4 a0 = *reinterpret_cast<const uint4*>(rec);
                         const uint4 a1 = *reinterpret_cast<const uint4*>(rec + 4);
                         const float2 ds = *reinterpret_cast<const float2*>(rec + 8);
@@ -175,12 +211,13 @@ template <int F, int BPL> inline size_t gemv_lds_bytes(int M, int K) {
     return (size_t)M * (K / QK / BPL) * gemv_geom<F, BPL>::REC_DW * 4;
 }
 
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool NT, bool SUMI, int ABL = 0>
+template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool NT, bool SUMI, int ABL = 0, bool DMA = false>
 hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
-    const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
+    size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
+    if (DMA) lds += ((size_t)RPB * (g.K / QK) * wfmt<F>::BB + 15) / 16 * 16;
     const int grid = (g.N + RPB - 1) / RPB;
-    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, NSTAGE, NT, SUMI, ABL>;
+    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, NSTAGE, NT, SUMI, ABL, DMA>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -63,21 +63,24 @@ static int run(int M, int N, int K) {
         fprintf(stderr, "quantized bytes differ from the oracle\n");
         return 1;
     }
-    double e2 = 0, r2 = 0, maxrel = 0;
+    // vs the oracle: only fp32 summation order differs -> NMSE ~1e-13; vs FP32: the reference's
+    // quantization error (4.5550e-3 recorded for M=1 N=K=4096)
+    double e2 = 0, r2 = 0, o2 = 0, o2b = 0, q2 = 0;
     for (int m = 0; m < M; ++m)
         for (int n = 0; n < N; ++n) {
             const double ref = c_ref[(size_t)m * N + n], got = c[(size_t)m * N + n], got2 = c2[(size_t)n * M + m];
-            maxrel = fmax(maxrel, fabs(got - ref) / (1e-3 + fabs(ref)));
-            maxrel = fmax(maxrel, fabs(got2 - ref) / (1e-3 + fabs(ref)));
+            o2 += (got - ref) * (got - ref);
+            o2b += (got2 - ref) * (got2 - ref);
+            q2 += ref * ref;
             const double f = c_fp32[(size_t)m * N + n];
             e2 += (got - f) * (got - f);
             r2 += f * f;
         }
-    printf("M=%d N=%d K=%d  max rel diff vs oracle %.3e  NMSE vs FP32 %.4e  (%s)\n", M, N, K, maxrel, e2 / r2,
-           qg_version());
-    hipFree(da); hipFree(db); hipFree(dc); hipFree(dc2); hipFree(dA); hipFree(dB);
-    hipStreamDestroy(st);
-    return (maxrel < 1e-4 && e2 / r2 < 5e-3) ? 0 : 1;
+    const double nm_o = fmax(o2, o2b) / q2;
+    printf("M=%d N=%d K=%d  NMSE vs oracle %.3e  NMSE vs FP32 %.4e  (%s)\n", M, N, K, nm_o, e2 / r2, qg_version());
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dc2); (void)hipFree(dA); (void)hipFree(dB);
+    (void)hipStreamDestroy(st);
+    return (nm_o < 1e-10 && e2 / r2 < 5e-3) ? 0 : 1;
 }
 
 int main() {

@@ -31,14 +31,14 @@ static uint16_t f2h(float f) {
     return b;
 }
 
-template <int BPL, int LPR, int WGS, bool NT, int ABL = 0>
+template <int BPL, int LPR, int WGS, bool NT, int ABL = 0, bool DMA = false>
 void run(const char* name, Bufs& bf, hipStream_t st, std::vector<float>& ref, bool first) {
-    constexpr int NST = (WGS >= 512 ? 4 : WGS == 256 ? 8 : WGS == 128 ? 16 : 32);
+    constexpr int NST = (WGS >= 1024 ? 2 : WGS >= 512 ? 4 : WGS == 256 ? 8 : WGS == 128 ? 16 : 32);
     GemmArgs g;
     g.A = bf.a; g.C = bf.c; g.M = 1; g.N = bf.N; g.K = bf.K; g.wtype = FMT_Q4_0; g.ldc_m = bf.N; g.ldc_n = 1;
     if (!gemv_shape_ok<FMT_Q4_0, BPL>(g)) { printf("%-22s skipped (shape)\n", name); return; }
     const int R = (int)bf.w.size();
-    auto launch = [&](int i) { g.B = bf.w[i % R]; CK((gemv_launch<FMT_Q4_0, 1, BPL, LPR, WGS, NST, NT, false, ABL>(g, st))); };
+    auto launch = [&](int i) { g.B = bf.w[i % R]; CK((gemv_launch<FMT_Q4_0, 1, BPL, LPR, WGS, NST, NT, false, ABL, DMA>(g, st))); };
     for (int i = 0; i < 2 * R; ++i) launch(i);
     CK(hipStreamSynchronize(st));
     // correctness vs the first variant (same copy 0)
@@ -98,23 +98,18 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&bf.c, N * 4));
     printf("N=%d K=%d weight bytes %.2f MB, %d copies\n", N, K, wbytes / 1e6, R);
     std::vector<float> ref;
-    run<8, 16, 256, false>("bpl8_lpr16_wg256", bf, st, ref, true);
-    run<8, 16, 512, false>("bpl8_lpr16_wg512", bf, st, ref, false);
-    run<8, 16, 128, false>("bpl8_lpr16_wg128", bf, st, ref, false);
-    run<8, 8, 256, false>("bpl8_lpr8_wg256", bf, st, ref, false);
-    run<4, 32, 256, false>("bpl4_lpr32_wg256", bf, st, ref, false);
-    run<4, 16, 256, false>("bpl4_lpr16_wg256", bf, st, ref, false);
-    run<4, 32, 512, false>("bpl4_lpr32_wg512", bf, st, ref, false);
-    run<2, 64, 256, false>("bpl2_lpr64_wg256", bf, st, ref, false);
-    run<2, 32, 256, false>("bpl2_lpr32_wg256", bf, st, ref, false);
+    run<4, 32, 512, false>("bpl4_lpr32_wg512", bf, st, ref, true);
     run<2, 64, 512, false>("bpl2_lpr64_wg512", bf, st, ref, false);
-    run<2, 16, 256, false>("bpl2_lpr16_wg256", bf, st, ref, false);
-    // ablations (timing only): 1 = no activation staging, 2 = no decode/dot, 3 = loads only
-    run<8, 16, 256, false, 1>("bpl8 abl1(no-stage)", bf, st, ref, false);
-    run<8, 16, 256, false, 2>("bpl8 abl2(no-dot)", bf, st, ref, false);
-    run<8, 16, 256, false, 3>("bpl8 abl3(loads)", bf, st, ref, false);
-    run<2, 64, 256, false, 1>("bpl2 abl1(no-stage)", bf, st, ref, false);
-    run<2, 64, 256, false, 2>("bpl2 abl2(no-dot)", bf, st, ref, false);
-    run<2, 64, 256, false, 3>("bpl2 abl3(loads)", bf, st, ref, false);
+    run<4, 32, 512, false, 0, true>("dma bpl4_lpr32_wg512", bf, st, ref, false);
+    run<4, 32, 256, false, 0, true>("dma bpl4_lpr32_wg256", bf, st, ref, false);
+    run<8, 16, 256, false, 0, true>("dma bpl8_lpr16_wg256", bf, st, ref, false);
+    run<8, 16, 512, false, 0, true>("dma bpl8_lpr16_wg512", bf, st, ref, false);
+    run<2, 64, 512, false, 0, true>("dma bpl2_lpr64_wg512", bf, st, ref, false);
+    run<2, 64, 256, false, 0, true>("dma bpl2_lpr64_wg256", bf, st, ref, false);
+    run<4, 32, 128, false, 0, true>("dma bpl4_lpr32_wg128", bf, st, ref, false);
+    run<8, 16, 1024, false, 0, true>("dma bpl8_lpr16_wg1024", bf, st, ref, false);
+    run<4, 32, 512, false, 2, true>("dma bpl4 abl2(no-dot)", bf, st, ref, false);
+    run<4, 32, 512, false, 3, true>("dma bpl4 abl3(loads)", bf, st, ref, false);
+    run<4, 32, 512, false, 3>("bpl4 abl3(loads)", bf, st, ref, false);
     return 0;
 }
