@@ -117,6 +117,25 @@ __device__ __forceinline__ int dot_block(const uint32_t* q, const uint32_t* a) {
     return s;
 }
 
+// Sum of x over each aligned group of G lanes (G = 1..64, a power of two), delivered in the LAST
+// lane of the group (other lanes hold partial sums). DPP row ops, no LDS round trips: xor-1 and
+// xor-2 quad permutes, row_shr 4 and 8 inside each 16-lane row, then row_bcast 15 / 31 across rows
+// (gfx9 DPP). The pairing order is fixed, so the result is deterministic.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF, false));
+}
+template <int G> __device__ __forceinline__ float group_sum_last(float x) {
+    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "power-of-two group");
+    if constexpr (G >= 2) x += dpp_f<0xB1>(x);        // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) x += dpp_f<0x4E>(x);        // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x += dpp_f<0x114>(x);       // row_shr:4
+    if constexpr (G >= 16) x += dpp_f<0x118>(x);      // row_shr:8
+    if constexpr (G >= 32) x += dpp_f<0x142, 0xA>(x); // row_bcast:15 into rows 1, 3
+    if constexpr (G >= 64) x += dpp_f<0x143, 0xC>(x); // row_bcast:31 into rows 2, 3
+    return x;
+}
+
 // Per-block fp32 term, operation order as in the reference (see header comment).
 template <int F> __device__ __forceinline__ float block_term(int sumi, float dw, float mw, float da, float sa) {
     const float fs = (float)sumi;
