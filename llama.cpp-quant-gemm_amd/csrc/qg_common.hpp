@@ -137,11 +137,14 @@ template <int G> __device__ __forceinline__ float group_sum_last(float x) {
 }
 
 // Per-block fp32 term, operation order as in the reference (see header comment).
-template <int F> __device__ __forceinline__ float block_term(int sumi, float dw, float mw, float da, float sa) {
-    const float fs = (float)sumi;
+// fs = (float)sumi (exact: |sumi| < 2^24).
+template <int F> __device__ __forceinline__ float block_term_f(float fs, float dw, float mw, float da, float sa) {
     if constexpr (F == FMT_Q4_0) return dw * (da * fs - 8.0f * sa);
     else if constexpr (F == FMT_Q5_0) return dw * (da * fs - 16.0f * sa);
     else return dw * da * fs + mw * sa;
+}
+template <int F> __device__ __forceinline__ float block_term(int sumi, float dw, float mw, float da, float sa) {
+    return block_term_f<F>((float)sumi, dw, mw, da, sa);
 }
 
 }  // namespace qg

@@ -1,0 +1,342 @@
+// qg_mmq_kernel.hpp — W4A8 prefill GEMM (M > 8) on the CDNA4 matrix cores, v_mfma_i32_16x16x32_i8.
+//
+// C[M,N] = A_q8_1[M,K] . B_w[N,K]^T (include/gemm_reference.h:175-222), activation-major.
+//
+// One MFMA = one Q-block: v_mfma_i32_16x16x32_i8 has K = 32, so each MFMA returns the exact int32
+// sumi of 16 (weight row n) x 16 (token m) pairs for one block. The per-block epilogue runs on the
+// VALU and is the kernel's real arithmetic cost at prefill sizes (one per (n, m, block)), so it is
+// cut to 3 ops per element: the accumulator is seeded with the bit pattern of 1.5*2^23, so the
+// MFMA's integer add leaves cf = 12582912.0f + sumi as a float (|sumi| < 2^22, no v_cvt_f32_i32);
+// fma(d_a, cf, -d_a*1.5*2^23) = round(d_a * sumi), bit-identical to the reference's d_a * fs (the
+// constant is exact in f32); minus 8 s_a (Q4_0) as in the reference; one fma into the accumulator
+// (inside the summation-order bound of the parity tests).
+//
+// Operand k-order: lane (r = lane&15, q = lane>>4) supplies, for its weight row / token r, the 8
+// bytes of k-slot q: elements 4q..4q+3 and 16+4q..16+4q+3 of the block. For the weights that is qs
+// dword q split into low / high nibbles (+ the qh bits for Q5_x); for the activations qs dwords q
+// and 4+q. A and B use the same slot -> element map and the integer sum is order-free.
+// C layout (gfx950, dtype-independent): lane holds column m = lane&15, rows n = 4q + e (e < 4), so
+// the token's scales are per-lane scalars and the 4 row scales come from a small LDS table.
+//
+// Tiling: a workgroup owns BN weight rows x 16*TT tokens and ALL of K; its W waves
+// split K into 128-element stages (4 blocks), wave w taking stages w, w+W, ... With BN = 16,
+// TT = 2 the M = 32, N = 4096 prefill is 256 workgroups, one per CU. Each wave streams its stages
+// with LDS-DMA (global_load_lds: no VGPR staging, lane-linear LDS images [row][4 blocks] and
+// [token][144 B]) into two wave-private LDS buffers, the next stage in flight while the current one
+// computes (counted vmcnt). No workgroup barrier in the main loop; the W partial tiles are summed
+// in fixed wave order through LDS at the end.
+//
+// MFMA results are read only after the next block's MFMAs have issued (software pipeline inside a
+// stage) or behind an explicit wait (the stage's last block): reading them with only the wait
+// states hipcc inserts for this instruction on gfx950 gave wrong sums on the GPU
+// (tools/mmq_debug.hip).
+#pragma once
+#include "qg_common.hpp"
+#include "qg_kernels.hpp"
+
+namespace qg {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int MMQ_BIAS = 0x4B400000;  // bits of 12582912.0f = 1.5 * 2^23
+constexpr float MMQ_BIAS_F = 12582912.0f;
+constexpr int MMQ_SB = 4;             // blocks per stage
+
+#ifdef QG_MMQ_STAMPS
+// diagnostic build only (tools/mmq_timeline.hip): per-wave s_memrealtime stamps
+__device__ unsigned long long g_mmq_stamps[8 * 65536];
+#define MMQ_STAMP(k) stamps[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MMQ_STAMP(k)
+#endif
+
+// 32 bits at byte offset (compile-time OFF) of an LDS row, from aligned dword reads.
+template <int OFF> __device__ __forceinline__ uint32_t lds32(const uint8_t* base) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (OFF & ~3));
+    if constexpr (OFF % 4 == 0) return p[0];
+    else return __builtin_amdgcn_alignbyte(p[1], p[0], OFF % 4);
+}
+
+// One LDS-DMA instruction: lane's SZ bytes at g -> LDS at (wave-uniform) l + lane * SZ. A __device__
+// function: called straight from a lambda inside the kernel, the builtin made the host pass drop
+// the kernel's launch stub without a diagnostic (undefined symbol at link time).
+template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t* l) {
+    auto gp = (const __attribute__((address_space(1))) void*)g;
+    auto lp = (__attribute__((address_space(3))) void*)l;
+    static_assert(SZ == 4 || SZ == 12 || SZ == 16, "global_load_lds sizes");
+    if constexpr (SZ == 16) __builtin_amdgcn_global_load_lds(gp, lp, 16, 0, 0);
+    else if constexpr (SZ == 12) __builtin_amdgcn_global_load_lds(gp, lp, 12, 0, 0);
+    else __builtin_amdgcn_global_load_lds(gp, lp, 4, 0, 0);
+}
+
+template <int F, int BN, int TT, int W> struct mmq_geom {
+    using T = wfmt<F>;
+    static constexpr int RSB = MMQ_SB * T::BB;                // weight bytes per row per stage
+    static constexpr int WPS = RSB % 16 == 0 ? 16 : 4;          // weight DMA piece (bytes)
+    static constexpr int WPC = BN * RSB / WPS;                 // weight pieces per stage
+    static constexpr int NWI = (WPC + 63) / 64;                // weight DMA instructions per stage
+    static constexpr int NTOK = 16 * TT;
+    static constexpr int APC = NTOK * 9;                       // activation 16-B pieces per stage
+    static constexpr int NAI = (APC + 63) / 64;                // activation DMA instructions per stage
+    static constexpr int NI = NWI + NAI;
+    static constexpr int RT = BN / 16;                         // row tiles
+    static constexpr int NMW = T::MOFF >= 0 ? 2 : 1;           // weight scale tables: d (and m)
+    // LDS buffer layout (bytes). Every DMA instruction runs on all 64 lanes (see issue()), so the
+    // weight and activation images are padded to whole instructions.
+    static constexpr int OFF_A = NWI * 64 * WPS;
+    static constexpr int OFF_WT = OFF_A + NAI * 64 * 16;
+    static constexpr int OFF_AT = OFF_WT + MMQ_SB * NMW * BN * 4;
+    static constexpr int BUF = OFF_AT + MMQ_SB * NTOK * 16;
+    static constexpr int NACC = RT * TT * 4;                   // accumulators per lane
+    // wave buffers; the end-of-kernel partial tiles reuse them (after a barrier)
+    static constexpr size_t LDS = (size_t)W * (2 * BUF > NACC * 256 ? 2 * BUF : NACC * 256);
+    static_assert(LDS <= 160 * 1024, "LDS per workgroup");
+    static_assert(OFF_WT % 16 == 0 && OFF_AT % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
+};
+
+template <int F, int BN, int TT, int W, bool SUMI>
+__global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                     float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
+                                                     int N, int K, long ldc_m, long ldc_n) {
+    using G = mmq_geom<F, BN, TT, W>;
+    using T = wfmt<F>;
+    static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int r16 = lane & 15;
+    const int q = lane >> 4;
+    const int n0 = blockIdx.x * BN;
+    const int m0 = blockIdx.y * G::NTOK;
+    const int nb = K / QK;
+    const int H = nb / MMQ_SB;  // stages
+    const long RB = (long)nb * T::BB;
+    const long AB = (long)nb * Q8_1_BYTES;
+    uint8_t* bufs = smem + wave * 2 * G::BUF;
+#ifdef QG_MMQ_STAMPS
+    unsigned long long stamps[8] = {};
+#endif
+    MMQ_STAMP(0);
+
+    // per-lane DMA source offsets within a stage (rows / tokens past the edge read the last valid
+    // one; their results are dropped)
+    int woff[G::NWI], aoff[G::NAI];
+#pragma unroll
+    for (int i = 0; i < G::NWI; ++i) {
+        const int p = min(64 * i + lane, G::WPC - 1);
+        const int row = p / (G::RSB / G::WPS);
+        woff[i] = (int)((long)min(n0 + row, N - 1) * RB) + (p - row * (G::RSB / G::WPS)) * G::WPS;
+    }
+#pragma unroll
+    for (int i = 0; i < G::NAI; ++i) {
+        const int p = min(64 * i + lane, G::APC - 1);
+        const int tok = p / 9;
+        aoff[i] = (int)((long)min(m0 + tok, M - 1) * AB) + (p - tok * 9) * 16;
+    }
+    // All lanes issue every DMA instruction (lanes past the image fetch a clamped piece into the
+    // padding): a lane-predicated global_load_lds let hipcc sink two of them into one block with a
+    // per-lane M0 base, read back with v_readfirstlane — wrong destinations for half the wave
+    // (found by tools/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
+    auto issue = [&](int h, uint8_t* buf) {
+        const uint8_t* wsrc = B + (long)h * G::RSB;
+        const uint8_t* asrc = A + (long)h * 144;
+#pragma unroll
+        for (int i = 0; i < G::NWI; ++i) glds<G::WPS>(wsrc + woff[i], buf + 64 * i * G::WPS);
+#pragma unroll
+        for (int i = 0; i < G::NAI; ++i) glds<16>(asrc + aoff[i], buf + G::OFF_A + 64 * i * 16);
+    };
+
+    float acc[G::NACC];
+#pragma unroll
+    for (int i = 0; i < G::NACC; ++i) acc[i] = 0.0f;
+    const v4i bias = {MMQ_BIAS, MMQ_BIAS, MMQ_BIAS, MMQ_BIAS};
+
+    // Scale tables of a staged stage, converted once per wave: weight d (and m) as f32
+    // [block][d|m][row]; activation {d_a, -d_a * 1.5*2^23, c * s_a} as f32x4 [block][token] with
+    // c = 8 (Q4_0), 16 (Q5_0) or 1 (Q4_1 / Q5_1: m_w * s_a).
+    auto prep = [&](uint8_t* buf) {
+        float* wt = reinterpret_cast<float*>(buf + G::OFF_WT);
+        float4* at = reinterpret_cast<float4*>(buf + G::OFF_AT);
+#pragma unroll
+        for (int j = lane; j < MMQ_SB * BN; j += 64) {
+            const int b = j / BN, row = j - b * BN;
+            const uint8_t* blk = buf + row * G::RSB + b * T::BB;
+            wt[b * G::NMW * BN + row] = h2f(*reinterpret_cast<const uint16_t*>(blk));
+            if constexpr (T::MOFF >= 0) wt[b * G::NMW * BN + BN + row] = h2f(*reinterpret_cast<const uint16_t*>(blk + T::MOFF));
+        }
+#pragma unroll
+        for (int j = lane; j < MMQ_SB * G::NTOK; j += 64) {
+            const int b = j / G::NTOK, tk = j - b * G::NTOK;
+            const uint32_t dsh = *reinterpret_cast<const uint32_t*>(buf + G::OFF_A + tk * 144 + b * Q8_1_BYTES);
+            const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
+            constexpr float cs = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : 1.0f;
+            at[j] = make_float4(da, -(da * MMQ_BIAS_F), cs * sa, 0.0f);
+        }
+    };
+
+    struct blk_t {
+        v4i c[G::RT][TT];
+        float4 dw[G::RT], mw[G::RT];
+        float4 as[TT];  // {d_a, -d_a * bias, c * s_a, -}
+    };
+    auto epilogue = [&](const blk_t& p, int h, int b) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i) {
+                const float dws[4] = {p.dw[i].x, p.dw[i].y, p.dw[i].z, p.dw[i].w};
+                const float mws[4] = {p.mw[i].x, p.mw[i].y, p.mw[i].z, p.mw[i].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ce = p.c[i][t][e];
+                    if constexpr (SUMI) {
+                        const int n = n0 + 16 * i + 4 * q + e, m = m0 + 16 * t + r16;
+                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * MMQ_SB + b] = ce - MMQ_BIAS;
+                    } else {
+                        const float cf = __int_as_float(ce);  // = 1.5*2^23 + sumi, exact
+                        float& a = acc[(i * TT + t) * 4 + e];
+                        if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0) {
+                            const float t1 = __builtin_fmaf(p.as[t].x, cf, p.as[t].y);  // round(d_a * sumi)
+                            const float t2 = t1 - p.as[t].z;                          // - 8 s_a / - 16 s_a
+                            a = __builtin_fmaf(dws[e], t2, a);
+                        } else {
+                            const float x = cf - MMQ_BIAS_F;                          // exact: = sumi
+                            const float t1 = dws[e] * p.as[t].x * x;                  // (d_w * d_a) * fs
+                            a += __builtin_fmaf(mws[e], p.as[t].z, t1);
+                        }
+                    }
+                }
+            }
+    };
+
+    // the 4 blocks of one staged stage: fragments, MFMAs, epilogues one block behind
+    auto compute = [&](uint8_t* buf, int h) {
+        const float* wt = reinterpret_cast<const float*>(buf + G::OFF_WT);
+        const float4* at = reinterpret_cast<const float4*>(buf + G::OFF_AT);
+        blk_t prev;
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+            constexpr int o = b * T::BB;
+            blk_t cur;
+            long afrag[G::RT], bfrag[TT];
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i) {
+                const uint8_t* wr = buf + (16 * i + r16) * G::RSB;
+                const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
+                uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+                if constexpr (T::QH >= 0) {
+                    const uint32_t qh = lds32<o + T::QH>(wr);
+                    lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
+                    hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
+                }
+                afrag[i] = (long)(((unsigned long)hi << 32) | lo);
+                cur.dw[i] = *reinterpret_cast<const float4*>(wt + b * G::NMW * BN + 16 * i + 4 * q);
+                if constexpr (T::MOFF >= 0) cur.mw[i] = *reinterpret_cast<const float4*>(wt + b * G::NMW * BN + BN + 16 * i + 4 * q);
+                else cur.mw[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * 144 + b * Q8_1_BYTES;
+                const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
+                const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
+                bfrag[t] = (long)(((unsigned long)qa1 << 32) | qa0);
+                cur.as[t] = at[b * G::NTOK + 16 * t + r16];
+            }
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i)
+                    cur.c[i][t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(afrag[i], bfrag[t], bias, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (b > 0) epilogue(prev, h, b - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            prev = cur;
+        });
+        // the stage's last block has no MFMA behind it: wait out the matrix pipe explicitly
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue(prev, h, MMQ_SB - 1);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    int k = 0;
+    if (wave < H) issue(wave, bufs);
+    for (int h = wave; h < H; h += W, ++k) {
+        uint8_t* cur = bufs + (k & 1) * G::BUF;
+        if (h + W < H) {
+            issue(h + W, bufs + ((k + 1) & 1) * G::BUF);   // next stage in flight during this one
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NI) : "memory");  // this stage's DMA landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#ifdef QG_MMQ_STAMPS
+        if (h == wave) MMQ_STAMP(1);
+#endif
+        prep(cur);
+        compute(cur, h);
+#ifdef QG_MMQ_STAMPS
+        if (h == wave) MMQ_STAMP(2);
+#endif
+    }
+    MMQ_STAMP(3);
+
+    if constexpr (!SUMI) {
+        // fixed-order sum of the W partial tiles, in the wave buffers once every wave is done
+        float* red = reinterpret_cast<float*>(smem);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < G::NACC; ++i) red[(wave * G::NACC + i) * 64 + lane] = acc[i];
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < G::NACC * 64; idx += W * 64) {
+            float v = red[idx];
+#pragma unroll
+            for (int ww = 1; ww < W; ++ww) v += red[ww * G::NACC * 64 + idx];
+            const int a = idx >> 6, ln = idx & 63;
+            const int e = a & 3, t = (a >> 2) % TT, i = (a >> 2) / TT;
+            const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
+            const int m = m0 + 16 * t + (ln & 15);
+            if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
+        }
+    }
+#ifdef QG_MMQ_STAMPS
+    MMQ_STAMP(4);
+    if (lane == 0) {
+        const int wv = (blockIdx.y * gridDim.x + blockIdx.x) * W + wave;
+        for (int kk = 0; kk < 5; ++kk) g_mmq_stamps[8 * wv + kk] = stamps[kk];
+    }
+#endif
+}
+
+// Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
+// rows and stages aligned to the DMA piece, 32-bit byte offsets.
+template <int F, int BN, int TT, int W>
+inline bool mmq_shape_ok(const GemmArgs& g) {
+    using G = mmq_geom<F, BN, TT, W>;
+    if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_SB) != 0) return false;
+    const long RB = (long)(g.K / QK) * wfmt<F>::BB, AB = (long)(g.K / QK) * Q8_1_BYTES;
+    if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
+    if (((uintptr_t)g.B % (G::WPS == 16 ? 16 : 4)) != 0 || RB % G::WPS != 0) return false;
+    if (RB * g.N >= (1L << 31) || AB * g.M >= (1L << 31)) return false;
+    return true;
+}
+
+template <int F, int BN, int TT, int W, bool SUMI>
+hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
+    using G = mmq_geom<F, BN, TT, W>;
+    const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
+    auto k = mmq_kernel<F, BN, TT, W, SUMI>;
+    if (G::LDS > 64 * 1024) {
+        static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
+        if (!attr_set) {
+            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+    }
+    hipLaunchKernelGGL(k, grid, dim3(W * 64), G::LDS, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.C, g.sumi, g.M,
+                       g.N, g.K, g.ldc_m, g.ldc_n);
+    return hipGetLastError();
+}
+
+}  // namespace qg
