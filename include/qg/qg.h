@@ -51,8 +51,8 @@ typedef enum {
 /* Kernel family selection for qg_gemm_w4a8_ex (QG_ALGO_AUTO picks by shape). */
 typedef enum {
     QG_ALGO_AUTO = 0,
-    QG_ALGO_GEMV = 1,    /* M <= 8: register-resident super-block decode + v_dot4 */
-    QG_ALGO_MFMA = 2,    /* M > 8: LDS-staged activations, v_mfma_i32_32x32x32_i8 per Q-block */
+    QG_ALGO_GEMV = 1,    /* M <= 8 (auto: M <= 4): register-resident block decode + v_dot4 */
+    QG_ALGO_MFMA = 2,    /* any M (auto: M >= 5), K % 128 == 0: v_mfma_i32_16x16x32_i8 per Q-block */
     QG_ALGO_GENERIC = 3  /* any K % 32 == 0, any alignment */
 } qg_algo;
 
@@ -78,6 +78,32 @@ int qg_gemm_q4_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int 
 int qg_gemm_q4_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
 int qg_gemm_q5_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
 int qg_gemm_q5_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+
+/* ---- fused activation quantization --------------------------------------
+ * Activation-major C[M][N] = Q8_1(X)[M][K] . B[N][K]^T for FP32 activations X[M][K] (dense rows),
+ * quantized as quantize_row_q8_1_ref (include/quantize.h:165-193): the results are bit-identical to
+ * qg_quantize_q8_1(X) followed by qg_gemm_w4a8 on the same stream.
+ *   M <= 4 (X 16-B aligned): ONE launch, the quantization runs in the GEMV prologue (the Q8_1
+ *     activations never go through HBM);
+ *   larger M with workspace_bytes >= qg_gemm_w4a8_f32_workspace_size(M, K): quantize into the
+ *     workspace (4-B aligned device memory), then the QG_ALGO_AUTO product;
+ *   larger M without a workspace: the fused GEMV over 8-row chunks (weights streamed per chunk).
+ * X only 4-B aligned is served through the workspace; without one it is QG_ERR_ALIGN. */
+size_t qg_gemm_w4a8_f32_workspace_size(int M, int K);
+int qg_gemm_w4a8_f32(const float* X, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream);
+
+/* Replaces gemm_q4_0_fp16_fused(weight, fp16_activation, output, M, N, K, stream)
+ * (kernels/gemm/gemm_fused.cuh:311-338), weight-major: out[M][N] = W_q4_0[M][K/32] .
+ * Q8_1(act[N][K])^T, act IEEE half [N tokens][K], quantized with the fused kernel's semantics
+ * (gemm_fused.cuh:76-143: tree-reduced amax/sum, id = 1/f16(d), q clamped to +-127) — race-free
+ * here. Same dispatch as qg_gemm_w4a8_f32 with M <-> N (tokens); the _ws form
+ * takes a workspace of qg_gemm_w4a8_f32_workspace_size(N, K) bytes. */
+int qg_gemm_q4_0_fp16_fused(const void* W, const void* act_f16, float* out, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_q4_0_fp16_fused_ws(const void* W, const void* act_f16, float* out, int M, int N, int K, void* workspace,
+                               size_t workspace_bytes, qg_stream_t stream);
+/* The fused kernel's FP16 -> Q8_1 quantizer on its own (k halves, multiple of 32). */
+int qg_quantize_q8_1_f16_fused(const void* x_f16, void* y, int64_t k, qg_stream_t stream);
 
 /* ---- quantizers (include/quantize.h:343-368; python/quant_gemm/csrc/gemm_ops.cu:146-202) ----
  * x: float[k] (k = total elements, multiple of 32), y: k/32 blocks of the named type.

@@ -20,9 +20,12 @@ int hip_status(hipError_t e) {
 
 bool is_weight_type(int t) { return t == QG_TYPE_Q4_0 || t == QG_TYPE_Q4_1 || t == QG_TYPE_Q5_0 || t == QG_TYPE_Q5_1; }
 
+// Crossover from tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
+// wins up to M = 4 (its LDS activation reads grow with M), the MFMA kernel from M = 5 on.
 int select_algo(const GemmArgs& g) {
-    if (gemv_eligible(g)) return QG_ALGO_GEMV;
+    if (g.M <= 4 && gemv_eligible(g)) return QG_ALGO_GEMV;
     if (mfma_eligible(g)) return QG_ALGO_MFMA;
+    if (gemv_eligible(g)) return QG_ALGO_GEMV;
     return QG_ALGO_GENERIC;
 }
 
@@ -90,9 +93,90 @@ int weight_major(int wtype, const void* W, const void* A, float* out, int M, int
     g.ldc_m = 1; g.ldc_n = N;
     return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)s);
 }
+size_t fused_workspace_bytes(int M, int K) { return M > 0 && K > 0 ? (size_t)M * (size_t)(K / 32) * 36 : 0; }
+
+// FP32 / FP16 activations (g.ain != AIN_Q8_1), dense rows of K elements. Small M: quantization
+// fused into the GEMV prologue, one launch. Larger M: quantize into the caller's workspace, then
+// the Q8_1 product (same bytes, so the same results); without a workspace, fused GEMV launches
+// over row chunks (the weights are streamed once per chunk).
+int run_fused(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st) {
+    if (g.M < 0 || g.N < 0) return QG_ERR_INVALID_ARG;
+    if (g.K <= 0 || g.K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(g.wtype)) return QG_ERR_UNSUPPORTED;
+    if (g.M == 0 || g.N == 0) return QG_OK;
+    if (!g.A || !g.B || !g.C) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)g.B & 1) != 0) return QG_ERR_ALIGN;
+    const size_t es = g.ain == AIN_F32 ? 4 : 2;
+    if (((uintptr_t)g.A & (es - 1)) != 0) return QG_ERR_ALIGN;
+    const bool vec_ok = ((uintptr_t)g.A & 15) == 0;
+    if (g.M <= 4 && vec_ok && gemv_eligible(g)) return hip_status(launch_gemv(g, st));
+    if (ws && ws_bytes >= fused_workspace_bytes(g.M, g.K)) {
+        if (((uintptr_t)ws & 3) != 0) return QG_ERR_ALIGN;
+        const int64_t nblocks = (int64_t)g.M * (g.K / 32);
+        const hipError_t e = g.ain == AIN_F32 ? launch_quantize(QG_TYPE_Q8_1, 0, (const float*)g.A, ws, nblocks, st)
+                                              : launch_quantize_f16_fused(g.A, ws, nblocks, st);
+        if (e != hipSuccess) return hip_status(e);
+        GemmArgs q = g;
+        q.ain = AIN_Q8_1;
+        q.A = ws;
+        return run_gemm(q, QG_ALGO_AUTO, st);
+    }
+    if (!vec_ok) return QG_ERR_ALIGN;
+    for (int rows : {8, 4, 2, 1}) {
+        GemmArgs c = g;
+        c.M = rows < g.M ? rows : g.M;
+        if (!gemv_eligible(c)) continue;
+        const long row_bytes = (long)g.K * (long)es;
+        const int full = g.M / c.M, rem = g.M - full * c.M;
+        if (full > 65535) return QG_ERR_UNSUPPORTED;
+        c.batch = full;
+        c.sA = (long)c.M * row_bytes;
+        c.sB = 0;
+        c.sC = (long)c.M * g.ldc_m;
+        hipError_t e = launch_gemv(c, st);
+        if (e != hipSuccess || rem == 0) return hip_status(e);
+        c.batch = 1;
+        c.A = (const uint8_t*)g.A + (long)full * c.sA;
+        c.C = g.C + (long)full * c.sC;
+        c.M = rem;
+        return hip_status(launch_gemv(c, st));
+    }
+    return QG_ERR_UNSUPPORTED;
+}
 }  // namespace
 
 extern "C" {
+
+size_t qg_gemm_w4a8_f32_workspace_size(int M, int K) { return fused_workspace_bytes(M, K); }
+
+int qg_gemm_w4a8_f32(const float* X, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream) {
+    GemmArgs g;
+    g.A = X; g.ain = AIN_F32; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    return run_fused(g, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qg_gemm_q4_0_fp16_fused_ws(const void* W, const void* act_f16, float* out, int M, int N, int K, void* workspace,
+                               size_t workspace_bytes, qg_stream_t stream) {
+    // Weight-major (M weight rows, N tokens) -> activation-major args, as weight_major().
+    GemmArgs g;
+    g.A = act_f16; g.ain = AIN_F16_FUSED; g.B = W; g.C = out; g.M = N; g.N = M; g.K = K; g.wtype = QG_TYPE_Q4_0;
+    g.ldc_m = 1; g.ldc_n = N;
+    return run_fused(g, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qg_gemm_q4_0_fp16_fused(const void* W, const void* act_f16, float* out, int M, int N, int K, qg_stream_t stream) {
+    return qg_gemm_q4_0_fp16_fused_ws(W, act_f16, out, M, N, K, nullptr, 0, stream);
+}
+
+int qg_quantize_q8_1_f16_fused(const void* x, void* y, int64_t k, qg_stream_t stream) {
+    if (k < 0 || k % 32 != 0) return QG_ERR_BAD_K;
+    if (k == 0) return QG_OK;
+    if (!x || !y) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)x & 1) != 0 || ((uintptr_t)y & 3) != 0) return QG_ERR_ALIGN;
+    return hip_status(launch_quantize_f16_fused(x, y, k / 32, (hipStream_t)stream));
+}
 
 int qg_gemm_w4a8_ex(const void* A, const void* B, float* C, int M, int N, int K, int wtype, int algo,
                     qg_stream_t stream) {

@@ -1,10 +1,11 @@
 // qg_gemm_mfma.hip — product instantiations and dispatch of the prefill (M > 8) MFMA kernel
 // (qg_mmq_kernel.hpp).
 //
-// Tile configuration from the sweep in tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe5.txt;
-// cold weights, one MI355X):
-//  * M <= 16: 16 weight rows x 16 tokens per workgroup, 8 waves splitting K (N=4096: 256 WGs)
-//  * M <= 64: 32 rows x 16 tokens, 8 waves
+// Tile configuration from the sweeps in tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
+// mmq_probe_smallm.txt; cold weights, one MI355X):
+//  * M <= 64: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
+//    >= 256 workgroups (one per CU; fewer re-reads of the activations), else 16
+//    (M=32, N=4096: 32 rows x 2 token tiles = 256 WGs; M=8, N=4096: 16 rows = 256 WGs)
 //  * M  > 64: 32 rows x 64 tokens, 4 waves (more reuse of each staged stage per MFMA)
 #include "qg_mmq_kernel.hpp"
 
@@ -17,15 +18,15 @@ template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hi
     return g.sumi ? mmq_launch<F, BN, TT, W, true>(g, st) : mmq_launch<F, BN, TT, W, false>(g, st);
 }
 
+inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
+
 template <int F> bool ok_f(const GemmArgs& g) {
-    if (g.M <= 16) return ok_cfg<F, 16, 1, 8>(g);
-    if (g.M <= 64) return ok_cfg<F, 32, 1, 8>(g);
+    if (g.M <= 64) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);
     return ok_cfg<F, 32, 4, 4>(g);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
-    if (g.M <= 16) return run_cfg<F, 16, 1, 8>(g, st);
-    if (g.M <= 64) return run_cfg<F, 32, 1, 8>(g, st);
+    if (g.M <= 64) return wide_rows(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 16, 1, 8>(g, st);
     return run_cfg<F, 32, 4, 4>(g, st);
 }
 }  // namespace

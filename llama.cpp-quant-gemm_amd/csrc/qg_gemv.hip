@@ -3,27 +3,34 @@
 // Configuration from the tuning sweeps (tools/gemv_probe.hip, profiles/r01_tuning/): 4-block units
 // (72 B for Q4_0), 32 lanes per row, 512-thread workgroups (one per CU at N=4096) fastest cold and
 // hot; short rows (K/32/4 < 32) 4 lanes per row; K/32 not a multiple of 4: 2-block units.
+// The fused-quantization variants (AIN_F32 / AIN_F16_FUSED) share the configuration.
 #include "qg_gemv_kernel.hpp"
 
 namespace qg {
 
 namespace {
-template <int F, int MT, bool SUMI>
+template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK;
     if (nb % 4 == 0) {
-        if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, 4 * MT, SUMI>(g, st);
-        return gemv_launch<F, MT, 4, 4, 256, 8 * MT, SUMI>(g, st);
+        if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, 4 * MT, SUMI, AIN>(g, st);
+        return gemv_launch<F, MT, 4, 4, 256, 8 * MT, SUMI, AIN>(g, st);
     }
-    return gemv_launch<F, MT, 2, 8, 256, 8 * MT, SUMI>(g, st);
+    return gemv_launch<F, MT, 2, 8, 256, 8 * MT, SUMI, AIN>(g, st);
+}
+
+template <int F, int AIN> hipError_t launch_m(const GemmArgs& g, hipStream_t st) {
+    if (g.M <= 1) return launch_staged<F, 1, false, AIN>(g, st);
+    if (g.M <= 2) return launch_staged<F, 2, false, AIN>(g, st);
+    if (g.M <= 4) return launch_staged<F, 4, false, AIN>(g, st);
+    return launch_staged<F, 8, false, AIN>(g, st);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
-    if (g.sumi) return launch_staged<F, 8, true>(g, st);
-    if (g.M <= 1) return launch_staged<F, 1, false>(g, st);
-    if (g.M <= 2) return launch_staged<F, 2, false>(g, st);
-    if (g.M <= 4) return launch_staged<F, 4, false>(g, st);
-    return launch_staged<F, 8, false>(g, st);
+    if (g.sumi) return launch_staged<F, 8, true, AIN_Q8_1>(g, st);
+    if (g.ain == AIN_F32) return launch_m<F, AIN_F32>(g, st);
+    if (g.ain == AIN_F16_FUSED) return launch_m<F, AIN_F16_FUSED>(g, st);
+    return launch_m<F, AIN_Q8_1>(g, st);
 }
 
 template <int F> bool ok_f(const GemmArgs& g) {

@@ -20,10 +20,16 @@
 //  * Per-lane partials (unit order, block order) are reduced across the row's LPR lanes with DPP
 //    row ops (group_sum_last: no LDS round trips — the ds_bpermute chain it replaced was ~0.1 us of
 //    a 4 us launch); the row's last lane stores. Deterministic.
+//  * AIN != 0 (fused activation quantization): A is FP32 (AIN_F32, quantized as
+//    quantize_row_q8_1_ref) or FP16 (AIN_F16_FUSED, as kernels/gemm/gemm_fused.cuh:76-143) [M][K];
+//    each thread quantizes whole 32-element blocks straight into the LDS records
+//    (qg_quant_block.hpp), so the records — and every output — are bit-identical to the two-step
+//    quantize + GEMV path. The first block's loads are issued before the weight stream.
 // Tuning record (probes, per-wave timelines, rejected designs): profiles/r01_tuning/README.md.
 #pragma once
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
+#include "qg_quant_block.hpp"
 
 namespace qg {
 
@@ -35,8 +41,32 @@ template <int F, int BPL> struct gemv_geom {
 };
 
 // ------------------------------------------------------------------------------------------------
-// NSTAGE: activation dwords per thread loaded before the weight stream.
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI>
+// Load the 32 activation values of block g (AIN_F32: 128 B, AIN_F16_FUSED: 64 B; 16-B aligned).
+template <int AIN> __device__ __forceinline__ void load_act_block(const uint8_t* __restrict__ X, int g, float (&v)[32]) {
+    if constexpr (AIN == AIN_F32) {
+        const float4* p = reinterpret_cast<const float4*>(X) + (long)g * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 t = p[i];
+            v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+        }
+    } else {
+        const uint4* p = reinterpret_cast<const uint4*>(X) + (long)g * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 t = p[i];
+            const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[8 * i + 2 * j] = h2f(w[j] & 0xFFFFu);
+                v[8 * i + 2 * j + 1] = h2f(w[j] >> 16);
+            }
+        }
+    }
+}
+
+// NSTAGE: activation dwords per thread loaded before the weight stream (AIN_Q8_1).
+template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI, int AIN = AIN_Q8_1>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                    int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
@@ -56,47 +86,69 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
     const int row = blockIdx.x * RPB + (tid >> 6) * RPW + lane / LPR;
     const bool row_ok = row < N;
 
-    // 1) activation staging loads first
-    const int tot = M * nb * 9;
-    uint32_t av[NSTAGE];
-#pragma unroll
-    for (int i = 0; i < NSTAGE; ++i) {
-        const int g = tid + i * WGS;
-        av[i] = g < tot ? A[g] : 0u;
-    }
-
-    // 2) weight stream: first unit of this lane
     const uint8_t* wrow = B + (long)(row_ok ? row : 0) * ((long)U * G::UB);
     auto load_unit = [&](uint32_t (&dst)[G::UDW], int u) {
         const uint32_t* p = reinterpret_cast<const uint32_t*>(wrow + (long)((row_ok && u < U) ? u : 0) * G::UB);
 #pragma unroll
         for (int v = 0; v < G::UDW; ++v) dst[v] = p[v];
     };
-    uint32_t cur[G::UDW];
-    load_unit(cur, lir);
-
-    // 3) activations -> LDS records (the first NSTAGE*WGS dwords were loaded above; a K too
-    //    large for that chunk stages the remainder here, after the weight stream is in flight)
-    auto stage = [&](int g, uint32_t v) {
-        const int blk = g / 9;
-        const int w = g - blk * 9;
+    auto rec_of = [&](int blk) {
         const int m = blk / nb;
         const int b = blk - m * nb;
         const int u = b / BPL;
-        const int rec = (m * U + u) * G::REC_DW + (b - u * BPL) * 12;
-        if (w == 0) {
-            lds[rec + 8] = __float_as_uint(h2f(v & 0xFFFFu));
-            lds[rec + 9] = __float_as_uint(h2f(v >> 16));
-        } else {
-            lds[rec + w - 1] = v;
-        }
+        return (m * U + u) * G::REC_DW + (b - u * BPL) * 12;
     };
+    uint32_t cur[G::UDW];
+
+    if constexpr (AIN == AIN_Q8_1) {
+        // 1) activation staging loads first
+        const int tot = M * nb * 9;
+        uint32_t av[NSTAGE];
 #pragma unroll
-    for (int i = 0; i < NSTAGE; ++i) {
-        const int g = tid + i * WGS;
-        if (g < tot) stage(g, av[i]);
+        for (int i = 0; i < NSTAGE; ++i) {
+            const int g = tid + i * WGS;
+            av[i] = g < tot ? A[g] : 0u;
+        }
+        // 2) weight stream: first unit of this lane
+        load_unit(cur, lir);
+        // 3) activations -> LDS records (the first NSTAGE*WGS dwords were loaded above; a K too
+        //    large for that chunk stages the remainder here, after the weight stream is in flight)
+        auto stage = [&](int g, uint32_t v) {
+            const int blk = g / 9;
+            const int w = g - blk * 9;
+            const int rec = rec_of(blk);
+            if (w == 0) {
+                lds[rec + 8] = __float_as_uint(h2f(v & 0xFFFFu));
+                lds[rec + 9] = __float_as_uint(h2f(v >> 16));
+            } else {
+                lds[rec + w - 1] = v;
+            }
+        };
+#pragma unroll
+        for (int i = 0; i < NSTAGE; ++i) {
+            const int g = tid + i * WGS;
+            if (g < tot) stage(g, av[i]);
+        }
+        for (int g = tid + NSTAGE * WGS; g < tot; g += WGS) stage(g, A[g]);
+    } else {
+        // Fused quantization: one thread per 32-element block, first block's loads in flight
+        // before the weight stream.
+        const uint8_t* X = reinterpret_cast<const uint8_t*>(A);
+        const int totb = M * nb;
+        float xv[32];
+        if (tid < totb) load_act_block<AIN>(X, tid, xv);
+        load_unit(cur, lir);
+        for (int g = tid; g < totb; g += WGS) {
+            if (g != tid) load_act_block<AIN>(X, g, xv);
+            uint32_t w[9];
+            if constexpr (AIN == AIN_F32) quantize_q8_1_block<0>(xv, w);
+            else quantize_q8_1_block_fp16_fused(xv, w);
+            uint32_t* r = lds + rec_of(g);
+            *reinterpret_cast<uint4*>(r) = make_uint4(w[1], w[2], w[3], w[4]);
+            *reinterpret_cast<uint4*>(r + 4) = make_uint4(w[5], w[6], w[7], w[8]);
+            *reinterpret_cast<float2*>(r + 8) = make_float2(h2f(w[0] & 0xFFFFu), h2f(w[0] >> 16));
+        }
     }
-    for (int g = tid + NSTAGE * WGS; g < tot; g += WGS) stage(g, A[g]);
     __syncthreads();
 
     float acc[MT];
@@ -158,18 +210,20 @@ template <int F, int BPL>
 inline bool gemv_shape_ok(const GemmArgs& g) {
     if (g.M < 1 || g.M > 8) return false;
     if (g.K % (QK * BPL) != 0) return false;
-    if (((uintptr_t)g.B & 3) != 0 || ((uintptr_t)g.A & 3) != 0) return false;
-    if (g.batch > 1 && ((g.sB & 3) != 0 || (g.sA & 3) != 0)) return false;
+    const int aal = g.ain == AIN_Q8_1 ? 3 : 15;  // fused: 16-B vector loads of the FP32/FP16 rows
+    if (((uintptr_t)g.B & 3) != 0 || ((uintptr_t)g.A & aal) != 0) return false;
+    if (g.batch > 1 && ((g.sB & 3) != 0 || (g.sA & aal) != 0)) return false;
+    if (g.sumi && g.ain != AIN_Q8_1) return false;
     if (g.M > 2 && gemv_lds_bytes<F, BPL>(g.M, g.K) > 96 * 1024) return false;
     return true;
 }
 
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI>
+template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI, int AIN = AIN_Q8_1>
 hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
-    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, NSTAGE, SUMI>;
+    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, NSTAGE, SUMI, AIN>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

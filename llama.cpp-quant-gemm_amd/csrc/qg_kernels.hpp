@@ -5,10 +5,14 @@
 
 namespace qg {
 
+// Activation input of a product: Q8_1 blocks, or FP32 / FP16 rows quantized inside the kernel.
+enum : int { AIN_Q8_1 = 0, AIN_F32 = 1, AIN_F16_FUSED = 2 };
+
 // One W4A8 product C = A_q8_1 * B_w^T, activation-major indices (m = activation row, n = weight
 // row); the output element (m, n) lives at C[m * ldc_m + n * ldc_n].
 struct GemmArgs {
-    const void* A = nullptr;     // block_q8_1 [M][K/32]
+    const void* A = nullptr;     // block_q8_1 [M][K/32] (ain == AIN_Q8_1), else float/half [M][K]
+    int ain = AIN_Q8_1;
     const void* B = nullptr;     // weight blocks [N][K/32] of type wtype
     float* C = nullptr;
     int32_t* sumi = nullptr;     // debug: per-block int32 dots [M][N][K/32] instead of C
@@ -32,6 +36,8 @@ hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
 
 // Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);
+// FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143).
+hipError_t launch_quantize_f16_fused(const void* x, void* y, int64_t nblocks, hipStream_t st);
 hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st);
 
 }  // namespace qg

@@ -11,16 +11,9 @@
 //   Q4_1 / Q5_0 / Q5_1  tests/framework/test_framework.cuh:256-367 (the repo's only quantizers)
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
+#include "qg_quant_block.hpp"
 
 namespace qg {
-
-__device__ __forceinline__ uint32_t f2h_bits(float f) {
-    // Materialise the fp32 value first: without this barrier the compiler folds a preceding fmul
-    // into a mixed-precision v_fma_mix (one rounding straight to f16), which differs from the
-    // reference's double rounding (f32 product, then __float2half RNE) at f16 ties.
-    asm volatile("" : "+v"(f));
-    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f);  // RNE, as __float2half
-}
 
 template <bool VEC> __device__ __forceinline__ void load32(const float* __restrict__ x, float (&v)[32]) {
     if constexpr (VEC) {
@@ -51,38 +44,30 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
     float v[32];
     load32<VEC>(x + ib * QK, v);
 
-    if constexpr (TYPE == FMT_Q8_1 || TYPE == FMT_Q8_0) {
-        float amax = 0.0f, sum = 0.0f;
+    if constexpr (TYPE == FMT_Q8_1) {
+        uint32_t w[9];
+        quantize_q8_1_block<VARIANT>(v, w);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);  // 36-B blocks stay 4-B aligned
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            amax = fmaxf(amax, fabsf(v[j]));
-            sum += v[j];
-        }
+        for (int i = 0; i < 9; ++i) dst[i] = w[i];
+    } else if constexpr (TYPE == FMT_Q8_0) {
+        float amax = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
         const float d = amax / 127.0f;
         const float id = d > 0.0f ? 1.0f / d : 0.0f;
         uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int sq = 0;
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            int t = (int)roundf(v[j] * id);
-            t = VARIANT == 1 ? max(-127, min(127, t)) : max(-128, min(127, t));
-            sq += t;
+            const int t = max(-128, min(127, (int)roundf(v[j] * id)));
             q[j / 4] |= ((uint32_t)t & 0xFFu) << (8 * (j & 3));
         }
-        if constexpr (TYPE == FMT_Q8_1) {
-            const float s = VARIANT == 1 ? (float)sq * d : sum;
-            uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);  // 36-B blocks stay 4-B aligned
-            dst[0] = f2h_bits(d) | (f2h_bits(s) << 16);
+        uint32_t w[9];
+        w[0] = f2h_bits(d) | ((q[0] & 0xFFFFu) << 16);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) dst[1 + i] = q[i];
-        } else {
-            uint32_t w[9];
-            w[0] = f2h_bits(d) | ((q[0] & 0xFFFFu) << 16);
-#pragma unroll
-            for (int i = 1; i < 8; ++i) w[i] = (q[i - 1] >> 16) | ((q[i] & 0xFFFFu) << 16);
-            w[8] = q[7] >> 16;
-            store_u16<34>(y + ib * 34, w);
-        }
+        for (int i = 1; i < 8; ++i) w[i] = (q[i - 1] >> 16) | ((q[i] & 0xFFFFu) << 16);
+        w[8] = q[7] >> 16;
+        store_u16<34>(y + ib * 34, w);
     } else if constexpr (TYPE == FMT_Q4_0 || TYPE == FMT_Q5_0) {
         float amax = 0.0f;
 #pragma unroll
@@ -169,6 +154,22 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
     }
 }
 
+// FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143), the
+// workspace producer of qg_gemm_q4_0_fp16_fused_ws for token counts beyond the fused GEMV.
+__global__ __launch_bounds__(256) void quantize_f16_fused_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ y,
+                                                                 int64_t nblocks) {
+    const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ib >= nblocks) return;
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = h2f(x[ib * QK + j]);
+    uint32_t w[9];
+    quantize_q8_1_block_fp16_fused(v, w);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dst[i] = w[i];
+}
+
 // Dequantize: x = (q - off) * d  or  q * d + m  (include/quantize.h:84-102, 140-150, 198-210).
 template <int TYPE>
 __global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, int64_t nblocks) {
@@ -234,6 +235,13 @@ hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64
         case FMT_Q5_1: return lq<FMT_Q5_1, 0>(x, y, nblocks, st);
     }
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_quantize_f16_fused(const void* x, void* y, int64_t nblocks, hipStream_t st) {
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(quantize_f16_fused_kernel, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, st,
+                       (const uint16_t*)x, (uint8_t*)y, nblocks);
+    return hipGetLastError();
 }
 
 hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st) {

@@ -184,6 +184,74 @@ def gemm_q5_1_q8_1(weight_q, activation_q, M: int, N: int, K: int) -> torch.Tens
     return _gemm_weight_major("qg_gemm_q5_1_q8_1", Q5_1, weight_q, activation_q, M, N, K)
 
 
+# ---------------------------------------------------------------------------- fused activation quantization
+def _workspace(rows: int, K: int, dev: torch.device):
+    nbytes = _lib.load().qg_gemm_w4a8_f32_workspace_size(rows, K)
+    return torch.empty((nbytes,), dtype=torch.uint8, device=dev)
+
+
+def gemm_w4a8_f32(x: torch.Tensor, weight_q: torch.Tensor, wtype: int = Q4_0, workspace: bool = True,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Activation-major C[M, N] = Q8_1(x)[M, K] . B_w[N, K]^T for FP32 x [M, K]: identical to
+    ``gemm_w4a8(quantize_q8_1(x), weight_q, ...)``. M <= 4: one launch, x quantized in the GEMV
+    prologue. Larger M: through a Q8_1 workspace (``workspace=True``, from torch's caching
+    allocator) or the fused GEMV per 8-row chunk (``workspace=False``)."""
+    _require(x.is_cuda, "Input must be a CUDA tensor")
+    _require(x.dtype == torch.float32 and x.dim() == 2, "x must be float32 [M, K]")
+    M, K = x.shape
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(wtype in (Q4_0, Q4_1, Q5_0, Q5_1), f"unsupported weight type {wtype}")
+    N = weight_q.numel() // ((K // 32) * BLOCK_BYTES[wtype]) if K else 0
+    _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
+    x = x.contiguous()
+    w = weight_q.contiguous()
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=w.device)
+    else:
+        _require(out.is_contiguous() and out.dtype == torch.float32 and out.numel() == M * N, "bad out tensor")
+    ws = _workspace(M, K, w.device) if (workspace and M > 4) else None
+    with torch.cuda.device(w.device):
+        _lib.check(_lib.load().qg_gemm_w4a8_f32(_ptr(x), _ptr(w), _ptr(out), M, N, K, wtype,
+                                                _ptr(ws) if ws is not None else None,
+                                                ws.numel() if ws is not None else 0, _stream(w.device)),
+                   "gemm_w4a8_f32")
+    return out
+
+
+def gemm_q4_0_fp16_fused(weight_q: torch.Tensor, fp16_activation: torch.Tensor, M: int, N: int, K: int,
+                         workspace: bool = True) -> torch.Tensor:
+    """Weight-major out[M, N] = W_q4_0[M, K] . Q8_1(act[N, K])^T with the FP16 activations quantized
+    inside the product (kernels/gemm/gemm_fused.cuh:311-338 gemm_q4_0_fp16_fused; quantizer
+    semantics of gemm_fused.cuh:76-143)."""
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _check_blocks(weight_q, "Weight", M, K, 18)
+    _require(fp16_activation.is_cuda and fp16_activation.dtype == torch.float16, "Activation must be CUDA float16")
+    _require(fp16_activation.numel() == N * K, f"Activation shape mismatch: expected {N * K} elements")
+    w = weight_q.contiguous()
+    a = fp16_activation.contiguous()
+    out = torch.empty((M, N), dtype=torch.float32, device=w.device)
+    ws = _workspace(N, K, w.device) if (workspace and N > 4) else None
+    with torch.cuda.device(w.device):
+        _lib.check(_lib.load().qg_gemm_q4_0_fp16_fused_ws(_ptr(w), _ptr(a), _ptr(out), M, N, K,
+                                                          _ptr(ws) if ws is not None else None,
+                                                          ws.numel() if ws is not None else 0, _stream(w.device)),
+                   "gemm_q4_0_fp16_fused")
+    return out
+
+
+def quantize_q8_1_f16_fused(x: torch.Tensor) -> torch.Tensor:
+    """FP16 [..., K] -> Q8_1 uint8 [..., K/32, 36] with the fused kernel's quantizer semantics."""
+    _require(x.is_cuda and x.dtype == torch.float16, "Input must be a CUDA float16 tensor")
+    K = x.size(-1)
+    _require(K % 32 == 0, f"Last dimension must be divisible by 32, got {K}")
+    x = x.contiguous()
+    out = torch.empty(tuple(x.shape[:-1]) + (K // 32, 36), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.load().qg_quantize_q8_1_f16_fused(_ptr(x), _ptr(out), x.numel(), _stream(x.device)),
+                   "quantize_q8_1_f16_fused")
+    return out
+
+
 def debug_sumi(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
                wtype: int = Q4_0, algo: int = ALGO_AUTO) -> torch.Tensor:
     """Per-block int32 dots [M, N, K/32] through the same decode path as ``algo``."""
@@ -212,5 +280,6 @@ __all__ = [
     "QK4_0", "QK8_1", "BLOCK_Q4_0_BYTES", "BLOCK_Q8_1_BYTES",
     "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
     "gemm_w4a8_batched", "debug_sumi", "select_algo", "version",
+    "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

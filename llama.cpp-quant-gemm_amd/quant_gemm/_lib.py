@@ -21,7 +21,7 @@ STATUS = {0: "ok", -1: "invalid argument", -2: "K must be a positive multiple of
           -5: "HIP launch error"}
 
 # exported symbols and their signatures (kept in sync with include/qg/qg.h; tests check both ways)
-P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+P, I, I64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
 SIGNATURES = {
     "qg_gemm_w4a8": ([P, P, P, I, I, I, I, P], I),
     "qg_gemm_w4a8_ex": ([P, P, P, I, I, I, I, I, P], I),
@@ -30,6 +30,11 @@ SIGNATURES = {
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_1_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_w4a8_f32_workspace_size": ([I, I], SZ),
+    "qg_gemm_w4a8_f32": ([P, P, P, I, I, I, I, P, SZ, P], I),
+    "qg_gemm_q4_0_fp16_fused": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q4_0_fp16_fused_ws": ([P, P, P, I, I, I, P, SZ, P], I),
+    "qg_quantize_q8_1_f16_fused": ([P, P, I64, P], I),
     "qg_quantize_q8_1": ([P, P, I64, P], I),
     "qg_quantize_q4_0": ([P, P, I64, P], I),
     "qg_quantize": ([I, I, P, P, I64, P], I),

@@ -46,6 +46,8 @@ def lib() -> ctypes.CDLL:
         for name in ("qgo_quantize_row_q4_0", "qgo_quantize_row_q8_0", "qgo_quantize_row_q8_1",
                      "qgo_quantize_q8_1_fw", "qgo_quantize_q4_1", "qgo_quantize_q5_0", "qgo_quantize_q5_1"):
             getattr(L, name).argtypes = [P, P, I64]
+        L.qgo_quantize_q8_1_fused_f16.argtypes = [P, P, I64]
+        L.qgo_gemm_q4_0_fp16_fused.argtypes = [P, P, P, I, I, I]
         L.qgo_dequantize.argtypes = [I, P, P, I64]
         L.qgo_gemm_fp32.argtypes = [P, P, P, I, I, I]
         L.qgo_gemm_w4a16.argtypes = [P, P, P, I, I, I]
@@ -88,6 +90,28 @@ def quantize(x: np.ndarray, t: int, variant: int = 0) -> np.ndarray:
     out = np.empty(x.shape[:-1] + (k // 32, BLOCK_BYTES[t]), np.uint8)
     fn = "qgo_quantize_q8_1_fw" if (t == Q8_1 and variant == 1) else _QUANT[t]
     getattr(lib(), fn)(_p(x), _p(out), x.size)
+    return out
+
+
+def quantize_q8_1_fused_f16(x: np.ndarray) -> np.ndarray:
+    """FP16 [..., K] -> Q8_1 uint8 [..., K/32, 36], kernels/gemm/gemm_fused.cuh:76-143 semantics."""
+    x = np.ascontiguousarray(x, np.float16)
+    k = x.shape[-1]
+    assert k % 32 == 0
+    out = np.empty(x.shape[:-1] + (k // 32, 36), np.uint8)
+    lib().qgo_quantize_q8_1_fused_f16(_p(x), _p(out), x.size)
+    return out
+
+
+def gemm_q4_0_fp16_fused(w_q: np.ndarray, act: np.ndarray) -> np.ndarray:
+    """Weight-major out[M][N] = W[M] . quant_fused(act[N])^T (kernels/gemm/gemm_fused.cuh:311-338)."""
+    w_q = np.ascontiguousarray(w_q, np.uint8)
+    act = np.ascontiguousarray(act, np.float16)
+    m, nb = w_q.shape[0], w_q.shape[1]
+    n, k = act.shape
+    assert nb * 32 == k and w_q.shape[2] == 18
+    out = np.empty((m, n), np.float32)
+    lib().qgo_gemm_q4_0_fp16_fused(_p(w_q), _p(act), _p(out), m, n, k)
     return out
 
 

@@ -14,6 +14,10 @@
  *   qgo_quantize_row_q8_1    include/quantize.h:165-193   (s = sum of the original floats)
  *   qgo_quantize_q8_1_fw     tests/framework/test_framework.cuh:195-225 (s = d * sum(q))
  *   qgo_quantize_q4_1/5_0/5_1 tests/framework/test_framework.cuh:256-367
+ *   qgo_quantize_q8_1_fused_f16 kernels/gemm/gemm_fused.cuh:76-143 (per-block semantics of the
+ *                            fused kernel's smem quantizer: tree-reduced amax/sum, id from the
+ *                            f16-rounded d, q clamped to +-127 — race-free restatement)
+ *   qgo_gemm_q4_0_fp16_fused kernels/gemm/gemm_fused.cuh:157-338 (weight-major out[M][N], N fp16 tokens)
  *   qgo_dequantize           include/quantize.h:84-102, 140-150, 198-210 + per-format formulas
  *   qgo_gemm_fp32            include/gemm_reference.h:38-58
  *   qgo_gemm_w4a16           include/gemm_reference.h:73-112
@@ -170,6 +174,36 @@ void qgo_quantize_q8_1_fw(const float* src, void* dstv, int64_t k) {
         }
         dst[b].d = qgo_f2h(scale);
         dst[b].s = qgo_f2h(sum_q * scale);
+    }
+}
+
+/* gemm_fused.cuh:76-143. Thread t < 32 holds x[t]; max/sum halve 16, 8, 4, 2 then lanes 0+1. */
+void qgo_quantize_q8_1_fused_f16(const uint16_t* src, void* dstv, int64_t k) {
+    qg_block_q8_1* dst = (qg_block_q8_1*)dstv;
+    for (int64_t b = 0; b < k / QG_QK; b++) {
+        float x[32], mx[32], sm[32];
+        for (int t = 0; t < 32; t++) {
+            x[t] = qgo_h2f(src[b * QG_QK + t]);
+            mx[t] = fabsf(x[t]);
+            sm[t] = x[t];
+        }
+        for (int h = 16; h >= 2; h /= 2)
+            for (int t = 0; t < h; t++) {
+                mx[t] = fmaxf(mx[t], mx[t + h]);
+                sm[t] += sm[t + h];
+            }
+        const float amax = fmaxf(mx[0], mx[1]);
+        const float sum = sm[0] + sm[1];
+        dst[b].d = qgo_f2h(amax / 127.0f);
+        dst[b].s = qgo_f2h(sum);
+        const float d = qgo_h2f(dst[b].d);
+        const float id = (d != 0.0f) ? 1.0f / d : 0.0f;
+        for (int t = 0; t < 32; t++) {
+            /* (int8_t)roundf(.) then clamp; |x*id| <= 127 * d/f16(d) < 127.07, so no wrap occurs */
+            int q = (int)roundf(x[t] * id);
+            q = q < -127 ? -127 : (q > 127 ? 127 : q);
+            dst[b].qs[t] = (int8_t)q;
+        }
     }
 }
 
@@ -415,6 +449,21 @@ void qgo_gemm_w4a8_mt(const void* A, const void* B, float* C, int M, int N, int 
         pthread_create(&th[i], NULL, gemm_rows, &jobs[i]);
     }
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+}
+
+/* gemm_fused.cuh:311-338: out[M][N] = W_q4_0[M][K/32] . quant_fused(act_f16[N][K])^T. The
+ * reference sums each output over lane-strided blocks then a warp tree; this sums in block order
+ * (same block terms, dw * (da * sumi - 8 * sa) at :265; outputs agree to summation order). */
+void qgo_gemm_q4_0_fp16_fused(const void* W, const uint16_t* act, float* out, int M, int N, int K) {
+    const int nb = K / QG_QK;
+    qg_block_q8_1* aq = (qg_block_q8_1*)malloc((size_t)N * nb * sizeof(qg_block_q8_1));
+    qgo_quantize_q8_1_fused_f16(act, aq, (int64_t)N * K);
+    float* c = (float*)malloc((size_t)N * M * sizeof(float));
+    qgo_gemm_w4a8(aq, W, c, NULL, N, M, K, T_Q4_0); /* c[N][M] activation-major */
+    for (int i = 0; i < M; i++)
+        for (int j = 0; j < N; j++) out[(size_t)i * N + j] = c[(size_t)j * M + i];
+    free(c);
+    free(aq);
 }
 
 void qgo_gemm_w8a8(const void* Av, const void* Bv, float* C, int M, int N, int K) {

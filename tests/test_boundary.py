@@ -61,7 +61,8 @@ def test_static_queries(lib):
     assert so.qg_version().decode().startswith("qg-mi355x")
     assert [so.qg_block_bytes(t) for t in (2, 3, 6, 7, 8, 9, 0)] == [18, 20, 22, 24, 34, 36, 0]
     assert so.qg_select_algo(1, 4096, 4096, 2) == 1      # decode -> GEMV
-    assert so.qg_select_algo(8, 4096, 4096, 6) == 1
+    assert so.qg_select_algo(4, 4096, 4096, 6) == 1      # small batch -> GEMV
+    assert so.qg_select_algo(8, 4096, 4096, 6) == 2      # M >= 5 -> MFMA
     assert so.qg_select_algo(32, 4096, 4096, 2) == 2     # prefill -> MFMA
     assert so.qg_select_algo(1, 4096, 4128, 2) == 3      # K/32 odd -> generic
     assert so.qg_select_algo(16, 64, 4128, 7) == 3
@@ -87,6 +88,18 @@ def test_validation_codes_without_launch(lib):
     assert so.qg_quantize(9, 0, fake, P(4098), 32, None) == -4               # Q8_1 blocks need 4-B alignment
     assert so.qg_quantize(9, 0, None, None, 0, None) == 0
     assert so.qg_dequantize(5, fake, fake, 32, None) == -3
+    # fused activation quantization
+    assert so.qg_gemm_w4a8_f32_workspace_size(3, 4096) == 3 * 128 * 36
+    assert so.qg_gemm_w4a8_f32_workspace_size(0, 4096) == 0
+    assert so.qg_gemm_w4a8_f32(fake, fake, fake, 1, 1, 33, 2, None, 0, None) == -2
+    assert so.qg_gemm_w4a8_f32(fake, fake, fake, 1, 1, 32, 9, None, 0, None) == -3
+    assert so.qg_gemm_w4a8_f32(P(4100), fake, fake, 1, 8, 4096, 2, None, 0, None) == -4  # no 16-B X, no workspace
+    assert so.qg_gemm_w4a8_f32(P(4098), fake, fake, 1, 8, 4096, 2, None, 0, None) == -4  # floats misaligned
+    assert so.qg_gemm_w4a8_f32(None, None, None, 0, 8, 4096, 2, None, 0, None) == 0
+    assert so.qg_gemm_q4_0_fp16_fused(fake, fake, fake, 8, 1, 48, None) == -2
+    assert so.qg_gemm_q4_0_fp16_fused(fake, P(4097), fake, 8, 1, 64, None) == -4          # odd half pointer
+    assert so.qg_quantize_q8_1_f16_fused(fake, fake, 31, None) == -2
+    assert so.qg_quantize_q8_1_f16_fused(fake, P(4098), 32, None) == -4
 
 
 def test_from_view_validation(lib):

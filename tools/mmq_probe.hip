@@ -31,9 +31,9 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     struct S { int F, M, N, K; };
-    const S shapes[] = {{FMT_Q4_0, 32, 4096, 4096}, {FMT_Q4_0, 16, 4096, 4096}, {FMT_Q4_0, 64, 4096, 4096},
-                        {FMT_Q4_0, 128, 4096, 4096}, {FMT_Q4_0, 512, 4096, 4096}, {FMT_Q5_1, 32, 4096, 4096},
-                        {FMT_Q4_0, 32, 4096, 14336}};
+    const S shapes[] = {{FMT_Q4_0, 2, 4096, 4096}, {FMT_Q4_0, 3, 4096, 4096}, {FMT_Q4_0, 4, 4096, 4096},
+                        {FMT_Q4_0, 6, 4096, 4096}, {FMT_Q4_0, 8, 4096, 4096}, {FMT_Q5_1, 4, 4096, 4096},
+                        {FMT_Q5_1, 8, 4096, 4096}, {FMT_Q4_0, 8, 4096, 14336}, {FMT_Q4_0, 8, 32000, 4096}};
     for (const S& s : shapes) {
         const int nb = s.K / 32, bb = block_bytes(s.F);
         const long wbytes = (long)s.N * nb * bb;
@@ -57,6 +57,7 @@ int main() {
         CK(hipMalloc(&a, ha.size())); CK(hipMemcpy(a, ha.data(), ha.size(), hipMemcpyHostToDevice));
         CK(hipMalloc(&c, (size_t)s.M * s.N * 4));
         std::vector<Variant> vs;
+        vs.push_back({"gemv (C-ABI algo 1)", [](const GemmArgs& g, hipStream_t st) { return qg_gemm_w4a8_ex(g.A, g.B, g.C, g.M, g.N, g.K, g.wtype, 1, (qg_stream_t)st) == 0 ? hipSuccess : hipErrorUnknown; }});
         vs.push_back({"product (C-ABI algo 2)", [](const GemmArgs& g, hipStream_t st) { return qg_gemm_w4a8_ex(g.A, g.B, g.C, g.M, g.N, g.K, g.wtype, 2, (qg_stream_t)st) == 0 ? hipSuccess : hipErrorUnknown; }});
 #define V(BN, TT, W, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         switch (g.wtype) { case FMT_Q4_0: return mmq_shape_ok<FMT_Q4_0, BN, TT, W>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false>(g, st) : hipErrorInvalidValue; \
