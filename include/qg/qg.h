@@ -60,11 +60,16 @@ typedef enum {
  * Replaces gemm_w4a8_{naive,tiled,dp4a,tiled_dp4a,vectorized_dp4a}(A, B, C, M, N, K, stream)
  * (include/gemm_cuda_naive.cuh:285-292, gemm_cuda_tiled.cuh:293-300, gemm_cuda_dp4a.cuh:409-444)
  * and is the device twin of gemm_w4a8_reference (include/gemm_reference.h:175-222).
- * A: block_q8_1[M][K/32]; B: blocks of `wtype` (Q4_0/Q4_1/Q5_0/Q5_1) [N][K/32]; C: float[M][N],
- * overwritten. M == 0 or N == 0 is a no-op. */
+ * A: block_q8_1[M][K/32]; B: blocks of `wtype` (Q4_0/Q4_1/Q5_0/Q5_1, or Q8_0 = W8A8) [N][K/32];
+ * C: float[M][N], overwritten. M == 0 or N == 0 is a no-op. */
 int qg_gemm_w4a8(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, qg_stream_t stream);
 int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, int algo,
                     qg_stream_t stream);
+
+/* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
+ * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of
+ * gemm_w8a8_reference (include/gemm_reference.h:233-267). Same as qg_gemm_w4a8(..., QG_TYPE_Q8_0). */
+int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream);
 
 /* Strided batch of independent products (e.g. the experts of an MoE layer, or several projections
  * sharing nothing): item i uses A + i*strideA, B + i*strideB (bytes) and C + i*strideC (floats).
@@ -78,6 +83,7 @@ int qg_gemm_q4_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int 
 int qg_gemm_q4_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
 int qg_gemm_q5_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
 int qg_gemm_q5_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_q8_0_q8_1(const void* W, const void* A_q8_1, float* out, int M, int N, int K, qg_stream_t stream);
 
 /* ---- fused activation quantization --------------------------------------
  * Activation-major C[M][N] = Q8_1(X)[M][K] . B[N][K]^T for FP32 activations X[M][K] (dense rows),
@@ -85,8 +91,9 @@ int qg_gemm_q5_1_q8_1(const void* W, const void* A_q8_1, float* out, int M, int 
  * qg_quantize_q8_1(X) followed by qg_gemm_w4a8 on the same stream.
  *   M <= 4 (X 16-B aligned): ONE launch, the quantization runs in the GEMV prologue (the Q8_1
  *     activations never go through HBM);
- *   larger M with workspace_bytes >= qg_gemm_w4a8_f32_workspace_size(M, K): quantize into the
- *     workspace (4-B aligned device memory), then the QG_ALGO_AUTO product;
+ *   otherwise (larger M, or a K the GEMV does not take), with workspace_bytes >=
+ *     qg_gemm_w4a8_f32_workspace_size(M, K): quantize into the workspace (4-B aligned device
+ *     memory), then the QG_ALGO_AUTO product;
  *   larger M without a workspace: the fused GEMV over 8-row chunks (weights streamed per chunk).
  * X only 4-B aligned is served through the workspace; without one it is QG_ERR_ALIGN. */
 size_t qg_gemm_w4a8_f32_workspace_size(int M, int K);

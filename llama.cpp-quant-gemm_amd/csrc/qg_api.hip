@@ -18,7 +18,9 @@ int hip_status(hipError_t e) {
     return QG_ERR_HIP;
 }
 
-bool is_weight_type(int t) { return t == QG_TYPE_Q4_0 || t == QG_TYPE_Q4_1 || t == QG_TYPE_Q5_0 || t == QG_TYPE_Q5_1; }
+bool is_weight_type(int t) {
+    return t == QG_TYPE_Q4_0 || t == QG_TYPE_Q4_1 || t == QG_TYPE_Q5_0 || t == QG_TYPE_Q5_1 || t == QG_TYPE_Q8_0;
+}
 
 // Crossover from tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
 // wins up to M = 4 (its LDS activation reads grow with M), the MFMA kernel from M = 5 on.
@@ -210,6 +212,13 @@ int qg_gemm_q5_0_q8_1(const void* W, const void* A, float* out, int M, int N, in
 }
 int qg_gemm_q5_1_q8_1(const void* W, const void* A, float* out, int M, int N, int K, qg_stream_t s) {
     return weight_major(QG_TYPE_Q5_1, W, A, out, M, N, K, s);
+}
+int qg_gemm_q8_0_q8_1(const void* W, const void* A, float* out, int M, int N, int K, qg_stream_t s) {
+    return weight_major(QG_TYPE_Q8_0, W, A, out, M, N, K, s);
+}
+
+int qg_gemm_w8a8(const void* A, const void* B, float* C, int M, int N, int K, qg_stream_t stream) {
+    return qg_gemm_w4a8_ex(A, B, C, M, N, K, QG_TYPE_Q8_0, QG_ALGO_AUTO, stream);
 }
 
 int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_stream_t stream) {

@@ -14,6 +14,7 @@
 //   Q4_1  d_w * d_a * sumi + m_w * s_a        flashinfer_trace/definitions/quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json:79
 //   Q5_1  d_w * d_a * sumi + m_w * s_a        (the reference's /4 at gemm_quant_formats.cuh:148,266 is a
 //                                              mis-port and is NOT reproduced; SURVEY.md §0 defect 2)
+//   Q8_0  sumi * d_a * d_w                    include/gemm_reference.h:260 (W8A8, gemm_w8a8_reference)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,12 +26,14 @@ namespace qg {
 // ggml_type ids (compat/ggml_types.h:199-215)
 enum : int { FMT_Q4_0 = 2, FMT_Q4_1 = 3, FMT_Q5_0 = 6, FMT_Q5_1 = 7, FMT_Q8_0 = 8, FMT_Q8_1 = 9 };
 
-// Field byte offsets inside one weight block; -1 = field absent.
+// Field byte offsets inside one weight block; -1 = field absent. Q8 = 32 signed bytes in element
+// order (Q8_0) instead of 16 nibble pairs.
 template <int F> struct wfmt;
-template <> struct wfmt<FMT_Q4_0> { static constexpr int BB = 18, MOFF = -1, QH = -1, QS = 2; };
-template <> struct wfmt<FMT_Q4_1> { static constexpr int BB = 20, MOFF = 2, QH = -1, QS = 4; };
-template <> struct wfmt<FMT_Q5_0> { static constexpr int BB = 22, MOFF = -1, QH = 2, QS = 6; };
-template <> struct wfmt<FMT_Q5_1> { static constexpr int BB = 24, MOFF = 2, QH = 4, QS = 8; };
+template <> struct wfmt<FMT_Q4_0> { static constexpr int BB = 18, MOFF = -1, QH = -1, QS = 2; static constexpr bool Q8 = false; };
+template <> struct wfmt<FMT_Q4_1> { static constexpr int BB = 20, MOFF = 2, QH = -1, QS = 4; static constexpr bool Q8 = false; };
+template <> struct wfmt<FMT_Q5_0> { static constexpr int BB = 22, MOFF = -1, QH = 2, QS = 6; static constexpr bool Q8 = false; };
+template <> struct wfmt<FMT_Q5_1> { static constexpr int BB = 24, MOFF = 2, QH = 4, QS = 8; static constexpr bool Q8 = false; };
+template <> struct wfmt<FMT_Q8_0> { static constexpr int BB = 34, MOFF = -1, QH = -1, QS = 2; static constexpr bool Q8 = true; };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -77,8 +80,9 @@ __device__ __forceinline__ uint32_t spread4_bit4(uint32_t x) {
     return ((uint32_t)__umul24(x, 0x00204081u) & 0x01010101u) << 4;
 }
 
-// Decoded weight block: q[i] = elements 4i..4i+3 (i<4) / 16+4(i-4).. (i>=4) as unsigned bytes,
-// exactly the stored values (no offset removed), plus its scale(s).
+// Decoded weight block: q[i] = elements 4i..4i+3 (i<4) / 16+4(i-4).. (i>=4), i.e. elements 4i..4i+3,
+// exactly the stored values (no offset removed; unsigned nibbles, or Q8_0's signed bytes), plus its
+// scale(s).
 struct wblock {
     uint32_t q[8];
     float d, m;
@@ -92,6 +96,10 @@ template <int F, int BI> __device__ __forceinline__ wblock decode_block(const ui
     r.d = h2f(ld16<base>(w));
     if constexpr (T::MOFF >= 0) r.m = h2f(ld16<base + T::MOFF>(w));
     else r.m = 0.0f;
+    if constexpr (T::Q8) {
+        static_for<8>([&](auto I) { r.q[decltype(I)::value] = ld32<base + T::QS + 4 * decltype(I)::value>(w); });
+        return r;
+    }
     uint32_t qh = 0;
     if constexpr (T::QH >= 0) qh = ld32<base + T::QH>(w);
     static_for<4>([&](auto I) {
@@ -141,6 +149,7 @@ template <int G> __device__ __forceinline__ float group_sum_last(float x) {
 template <int F> __device__ __forceinline__ float block_term_f(float fs, float dw, float mw, float da, float sa) {
     if constexpr (F == FMT_Q4_0) return dw * (da * fs - 8.0f * sa);
     else if constexpr (F == FMT_Q5_0) return dw * (da * fs - 16.0f * sa);
+    else if constexpr (F == FMT_Q8_0) return fs * da * dw;
     else return dw * da * fs + mw * sa;
 }
 template <int F> __device__ __forceinline__ float block_term(int sumi, float dw, float mw, float da, float sa) {

@@ -44,6 +44,7 @@ bool gemv_eligible(const GemmArgs& g) {
         case FMT_Q4_1: return ok_f<FMT_Q4_1>(g);
         case FMT_Q5_0: return ok_f<FMT_Q5_0>(g);
         case FMT_Q5_1: return ok_f<FMT_Q5_1>(g);
+        case FMT_Q8_0: return ok_f<FMT_Q8_0>(g);
     }
     return false;
 }
@@ -54,6 +55,7 @@ hipError_t launch_gemv(const GemmArgs& g, hipStream_t st) {
         case FMT_Q4_1: return launch_f<FMT_Q4_1>(g, st);
         case FMT_Q5_0: return launch_f<FMT_Q5_0>(g, st);
         case FMT_Q5_1: return launch_f<FMT_Q5_1>(g, st);
+        case FMT_Q8_0: return launch_f<FMT_Q8_0>(g, st);
     }
     return hipErrorInvalidValue;
 }

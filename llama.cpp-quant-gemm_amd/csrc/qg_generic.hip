@@ -16,6 +16,13 @@ __device__ __forceinline__ void decode_bytes(const uint8_t* blk, uint32_t (&q)[8
     d = h2f((uint32_t)blk[0] | ((uint32_t)blk[1] << 8));
     m = 0.0f;
     if constexpr (T::MOFF >= 0) m = h2f((uint32_t)blk[T::MOFF] | ((uint32_t)blk[T::MOFF + 1] << 8));
+    if constexpr (T::Q8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            q[i] = (uint32_t)blk[T::QS + 4 * i] | ((uint32_t)blk[T::QS + 4 * i + 1] << 8) |
+                   ((uint32_t)blk[T::QS + 4 * i + 2] << 16) | ((uint32_t)blk[T::QS + 4 * i + 3] << 24);
+        return;
+    }
     uint32_t qh = 0;
     if constexpr (T::QH >= 0)
         qh = (uint32_t)blk[T::QH] | ((uint32_t)blk[T::QH + 1] << 8) | ((uint32_t)blk[T::QH + 2] << 16) |
@@ -94,6 +101,7 @@ hipError_t launch_generic(const GemmArgs& g, hipStream_t st) {
         case FMT_Q4_1: return launch_g<FMT_Q4_1>(g, st);
         case FMT_Q5_0: return launch_g<FMT_Q5_0>(g, st);
         case FMT_Q5_1: return launch_g<FMT_Q5_1>(g, st);
+        case FMT_Q8_0: return launch_g<FMT_Q8_0>(g, st);
     }
     return hipErrorInvalidValue;
 }

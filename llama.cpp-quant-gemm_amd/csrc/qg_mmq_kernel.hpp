@@ -13,8 +13,8 @@
 //
 // Operand k-order: lane (r = lane&15, q = lane>>4) supplies, for its weight row / token r, the 8
 // bytes of k-slot q: elements 4q..4q+3 and 16+4q..16+4q+3 of the block. For the weights that is qs
-// dword q split into low / high nibbles (+ the qh bits for Q5_x); for the activations qs dwords q
-// and 4+q. A and B use the same slot -> element map and the integer sum is order-free.
+// dword q split into low / high nibbles (+ the qh bits for Q5_x), for Q8_0 its signed qs dwords q and
+// 4+q; for the activations qs dwords q and 4+q. Q8_0 (W8A8) runs the Q4_0 epilogue with no s_a term. A and B use the same slot -> element map and the integer sum is order-free.
 // C layout (gfx950, dtype-independent): lane holds column m = lane&15, rows n = 4q + e (e < 4), so
 // the token's scales are per-lane scalars and the 4 row scales come from a small LDS table.
 //
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
             const int b = j / G::NTOK, tk = j - b * G::NTOK;
             const uint32_t dsh = *reinterpret_cast<const uint32_t*>(buf + G::OFF_A + tk * 144 + b * Q8_1_BYTES);
             const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
-            constexpr float cs = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : 1.0f;
+            constexpr float cs = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : 1.0f;
             at[j] = make_float4(da, -(da * MMQ_BIAS_F), cs * sa, 0.0f);
         }
     };
@@ -196,9 +196,9 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
                     } else {
                         const float cf = __int_as_float(ce);  // = 1.5*2^23 + sumi, exact
                         float& a = acc[(i * TT + t) * 4 + e];
-                        if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0) {
+                        if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0 || F == FMT_Q8_0) {
                             const float t1 = __builtin_fmaf(p.as[t].x, cf, p.as[t].y);  // round(d_a * sumi)
-                            const float t2 = t1 - p.as[t].z;                          // - 8 s_a / - 16 s_a
+                            const float t2 = t1 - p.as[t].z;                          // - 8 s_a / - 16 s_a / - 0
                             a = __builtin_fmaf(dws[e], t2, a);
                         } else {
                             const float x = cf - MMQ_BIAS_F;                          // exact: = sumi
@@ -223,8 +223,15 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RSB;
-                const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
-                uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+                uint32_t lo, hi;
+                if constexpr (T::Q8) {  // signed bytes, elements 4q.. and 16+4q..
+                    lo = lds32<o + T::QS>(wr + 4 * q);
+                    hi = lds32<o + T::QS + 16>(wr + 4 * q);
+                } else {
+                    const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
+                    lo = v & 0x0F0F0F0Fu;
+                    hi = (v >> 4) & 0x0F0F0F0Fu;
+                }
                 if constexpr (T::QH >= 0) {
                     const uint32_t qh = lds32<o + T::QH>(wr);
                     lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);

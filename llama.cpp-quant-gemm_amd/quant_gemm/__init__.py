@@ -34,6 +34,7 @@ BLOCK_Q8_1_BYTES = 36
 Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1 = 2, 3, 6, 7, 8, 9
 BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q5_0: 22, Q5_1: 24, Q8_0: 34, Q8_1: 36}
 ALGO_AUTO, ALGO_GEMV, ALGO_MFMA, ALGO_GENERIC = 0, 1, 2, 3
+WEIGHT_TYPES = (Q4_0, Q4_1, Q5_0, Q5_1, Q8_0)
 
 
 def _require(cond: bool, msg: str) -> None:
@@ -116,7 +117,7 @@ def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int
     """Activation-major C[M, N] = A_q8_1[M, K] . B_w[N, K]^T (include/gemm_reference.h:175-222;
     include/llama_adapter.h). M = tokens, N = weight rows."""
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
-    _require(wtype in (Q4_0, Q4_1, Q5_0, Q5_1), f"unsupported weight type {wtype}")
+    _require(wtype in WEIGHT_TYPES, f"unsupported weight type {wtype}")
     _check_blocks(activation_q, "Activation", M, K, 36)
     _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
     a = activation_q.contiguous()
@@ -194,13 +195,13 @@ def gemm_w4a8_f32(x: torch.Tensor, weight_q: torch.Tensor, wtype: int = Q4_0, wo
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """Activation-major C[M, N] = Q8_1(x)[M, K] . B_w[N, K]^T for FP32 x [M, K]: identical to
     ``gemm_w4a8(quantize_q8_1(x), weight_q, ...)``. M <= 4: one launch, x quantized in the GEMV
-    prologue. Larger M: through a Q8_1 workspace (``workspace=True``, from torch's caching
+    prologue. Larger M (or a K the GEMV does not take): through a Q8_1 workspace (``workspace=True``, from torch's caching
     allocator) or the fused GEMV per 8-row chunk (``workspace=False``)."""
     _require(x.is_cuda, "Input must be a CUDA tensor")
     _require(x.dtype == torch.float32 and x.dim() == 2, "x must be float32 [M, K]")
     M, K = x.shape
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
-    _require(wtype in (Q4_0, Q4_1, Q5_0, Q5_1), f"unsupported weight type {wtype}")
+    _require(wtype in WEIGHT_TYPES, f"unsupported weight type {wtype}")
     N = weight_q.numel() // ((K // 32) * BLOCK_BYTES[wtype]) if K else 0
     _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
     x = x.contiguous()
@@ -209,7 +210,7 @@ def gemm_w4a8_f32(x: torch.Tensor, weight_q: torch.Tensor, wtype: int = Q4_0, wo
         out = torch.empty((M, N), dtype=torch.float32, device=w.device)
     else:
         _require(out.is_contiguous() and out.dtype == torch.float32 and out.numel() == M * N, "bad out tensor")
-    ws = _workspace(M, K, w.device) if (workspace and M > 4) else None
+    ws = _workspace(M, K, w.device) if workspace else None
     with torch.cuda.device(w.device):
         _lib.check(_lib.load().qg_gemm_w4a8_f32(_ptr(x), _ptr(w), _ptr(out), M, N, K, wtype,
                                                 _ptr(ws) if ws is not None else None,
@@ -230,7 +231,7 @@ def gemm_q4_0_fp16_fused(weight_q: torch.Tensor, fp16_activation: torch.Tensor, 
     w = weight_q.contiguous()
     a = fp16_activation.contiguous()
     out = torch.empty((M, N), dtype=torch.float32, device=w.device)
-    ws = _workspace(N, K, w.device) if (workspace and N > 4) else None
+    ws = _workspace(N, K, w.device) if workspace else None
     with torch.cuda.device(w.device):
         _lib.check(_lib.load().qg_gemm_q4_0_fp16_fused_ws(_ptr(w), _ptr(a), _ptr(out), M, N, K,
                                                           _ptr(ws) if ws is not None else None,
@@ -250,6 +251,16 @@ def quantize_q8_1_f16_fused(x: torch.Tensor) -> torch.Tensor:
         _lib.check(_lib.load().qg_quantize_q8_1_f16_fused(_ptr(x), _ptr(out), x.numel(), _stream(x.device)),
                    "quantize_q8_1_f16_fused")
     return out
+
+
+def gemm_q8_0_q8_1(weight_q, activation_q, M: int, N: int, K: int) -> torch.Tensor:
+    """W8A8, weight-major (kernels/gemm/gemm_quant_formats.cuh:415-428)."""
+    return _gemm_weight_major("qg_gemm_q8_0_q8_1", Q8_0, weight_q, activation_q, M, N, K)
+
+
+def gemm_w8a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """W8A8, activation-major C[M, N] = A_q8_1 . B_q8_0^T (include/gemm_reference.h:233-267)."""
+    return gemm_w4a8(activation_q, weight_q, M, N, K, wtype=Q8_0)
 
 
 def debug_sumi(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
@@ -280,6 +291,6 @@ __all__ = [
     "QK4_0", "QK8_1", "BLOCK_Q4_0_BYTES", "BLOCK_Q8_1_BYTES",
     "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
     "gemm_w4a8_batched", "debug_sumi", "select_algo", "version",
-    "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused",
+    "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused", "gemm_w8a8", "gemm_q8_0_q8_1",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

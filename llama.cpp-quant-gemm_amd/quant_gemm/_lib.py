@@ -30,6 +30,8 @@ SIGNATURES = {
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_1_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q8_0_q8_1": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_w8a8": ([P, P, P, I, I, I, P], I),
     "qg_gemm_w4a8_f32_workspace_size": ([I, I], SZ),
     "qg_gemm_w4a8_f32": ([P, P, P, I, I, I, I, P, SZ, P], I),
     "qg_gemm_q4_0_fp16_fused": ([P, P, P, I, I, I, P], I),

@@ -154,6 +154,15 @@ def gemm_w4a8_mt(a_q, b_q, t: int = Q4_0, nthreads: int = 1) -> np.ndarray:
     return c
 
 
+def gemm_w8a8(a_q: np.ndarray, b_q: np.ndarray) -> np.ndarray:
+    """include/gemm_reference.h:233-267: Q8_1 activations x Q8_0 weights."""
+    m, nb = a_q.shape[0], a_q.shape[1]
+    n = b_q.shape[0]
+    c = np.empty((m, n), np.float32)
+    lib().qgo_gemm_w8a8(_p(np.ascontiguousarray(a_q)), _p(np.ascontiguousarray(b_q)), _p(c), m, n, nb * 32)
+    return c
+
+
 def gemm_w4a16(a: np.ndarray, b_q: np.ndarray) -> np.ndarray:
     m, k = a.shape
     n = b_q.shape[0]
@@ -196,6 +205,8 @@ def block_terms(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_
         return dw * (da * fs - np.float32(8.0) * sa)
     if t == Q5_0:
         return dw * (da * fs - np.float32(16.0) * sa)
+    if t == Q8_0:
+        return fs * da * dw
     mw = _h(b_q[..., 2:4])[None, :, :]
     return dw * da * fs + mw * sa
 

@@ -25,7 +25,7 @@
  *                            same loop with the corrected block formulas of
  *                            kernels/gemm/gemm_quant_formats.cuh:105-267 (no /4, SURVEY.md §0.2;
  *                            Q4_1 as flashinfer_trace/.../w4_1a8_q4_1_q8_1_n4096_k4096.json:79)
- *   qgo_gemm_w8a8            include/gemm_reference.h:233-267
+ *   qgo_gemm_w8a8            include/gemm_reference.h:233-267 (also qgo_gemm_w4a8 with t = Q8_0)
  *   qgo_vec_dot_q4_0_q8_1    include/gemm_reference.h:276-306
  *   qgo_dot4                 __dp4a semantics, include/gemm_cuda_dp4a.cuh:67-77
  */
@@ -304,6 +304,11 @@ static void weight_block(int t, const uint8_t* blk, int q[32], float* d, float* 
     uint16_t dh, mh = 0;
     memcpy(&dh, blk, 2);
     *d = qgo_h2f(dh);
+    if (t == T_Q8_0) { /* signed bytes in element order */
+        for (int j = 0; j < 32; j++) q[j] = (int8_t)blk[2 + j];
+        *m = 0.0f;
+        return;
+    }
     int qs_off = 2, qh_off = -1;
     if (t == T_Q4_1) { memcpy(&mh, blk + 2, 2); qs_off = 4; }
     if (t == T_Q5_0) { qh_off = 2; qs_off = 6; }
@@ -398,6 +403,7 @@ static int32_t block_sumi(const int q[32], const int8_t* aq) {
 static float block_term(int t, int32_t sumi, float dw, float mw, float da, float sa) {
     if (t == T_Q4_0) return dw * (da * sumi - 8.0f * sa);
     if (t == T_Q5_0) return dw * (da * sumi - 16.0f * sa);
+    if (t == T_Q8_0) return sumi * da * dw; /* gemm_reference.h:260 */
     return dw * da * sumi + mw * sa; /* Q4_1 / Q5_1 */
 }
 

@@ -77,7 +77,7 @@ def test_validation_codes_without_launch(lib):
     assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 33, 2, None) == -2        # bad K
     assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 0, 2, None) == -2
     assert so.qg_gemm_w4a8(fake, fake, fake, -1, 1, 32, 2, None) == -1       # negative M
-    assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 32, 8, None) == -3        # Q8_0 weights: not on this path
+    assert so.qg_gemm_w4a8(fake, fake, fake, 1, 1, 32, 9, None) == -3        # Q8_1 weights: not a weight format
     assert so.qg_gemm_w4a8(None, fake, fake, 1, 1, 32, 2, None) == -1        # null
     assert so.qg_gemm_w4a8(None, None, None, 0, 5, 64, 2, None) == 0         # empty: no-op
     assert so.qg_gemm_w4a8(fake, P(4097), fake, 1, 1, 32, 2, None) == -4     # odd weight pointer

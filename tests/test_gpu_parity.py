@@ -19,7 +19,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-WTYPES = [2, 3, 6, 7]
+WTYPES = [2, 3, 6, 7, 8]  # Q4_0, Q4_1, Q5_0, Q5_1, Q8_0 (W8A8)
 ALGOS = {"gemv": 1, "mfma": 2, "generic": 3}
 
 
@@ -181,7 +181,7 @@ def test_misaligned_weights_take_generic_path(O, qg):
 
 
 @pytest.mark.parametrize("t,sym", [(2, "gemm_q4_0_q8_1"), (3, "gemm_q4_1_q8_1"), (6, "gemm_q5_0_q8_1"),
-                                   (7, "gemm_q5_1_q8_1")])
+                                   (7, "gemm_q5_1_q8_1"), (8, "gemm_q8_0_q8_1")])
 @pytest.mark.parametrize("ntok", [1, 2, 6])
 def test_weight_major_api(O, qg, t, sym, ntok):
     """python/quant_gemm convention: out[M_w, N_tok] = W @ A^T (kernels/gemm/gemm_quant_formats.cuh:312)."""
@@ -190,6 +190,16 @@ def test_weight_major_api(O, qg, t, sym, ntok):
     out = host(getattr(qg, sym)(dev(wq), dev(aq), mw, ntok, k))
     assert out.shape == (mw, ntok)
     assert_close_to_oracle(O, np.ascontiguousarray(out.T), aq, wq, t)
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 4096, 4096), (3, 100, 1024), (32, 256, 2048), (5, 64, 96)])
+def test_w8a8_matches_gemm_w8a8_reference(O, qg, m, n, k):
+    """W8A8 (include/gemm_reference.h:233-267) through qg_gemm_w8a8, every dispatch branch."""
+    a, b, aq, bq = make_case(O, m, n, k, O.Q8_0)
+    c = host(qg.gemm_w8a8(dev(aq), dev(bq), m, n, k))
+    c_ref = assert_close_to_oracle(O, c, aq, bq, O.Q8_0)
+    assert np.array_equal(c_ref, O.gemm_w8a8(aq, bq))
+    assert O.nmse(c, O.gemm_fp32(a, b)) <= 1e-4
 
 
 def test_reference_harness_convention(O, qg):

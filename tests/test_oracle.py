@@ -164,3 +164,55 @@ def test_dequantize_roundtrip(O):
     for t in (2, 3, 6, 7, 8, 9):
         x = O.dequantize(O.quantize(b, t), t)
         assert np.abs(x - b).max() < {2: 0.08, 3: 0.075, 6: 0.04, 7: 0.04, 8: 0.005, 9: 0.005}[t]
+
+
+def test_w8a8_oracle_paths_agree(O):
+    """qgo_gemm_w4a8 with Q8_0 weights == the separate gemm_w8a8_reference restatement, bitwise."""
+    a, b = O.fill_uniform_step4(3, 64, 1024)
+    aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, O.Q8_0)
+    c = O.gemm_w4a8(aq, bq, O.Q8_0)
+    assert np.array_equal(c, O.gemm_w8a8(aq, bq))
+    assert O.nmse(c, O.gemm_fp32(a, b)) < 1e-4
+
+
+def _fused_f16_quantize_numpy(x16: np.ndarray) -> np.ndarray:
+    """Independent numpy restatement of kernels/gemm/gemm_fused.cuh:76-143 for one row."""
+    f32 = np.float32
+    out = np.zeros((x16.size // 32, 36), np.uint8)
+    for b in range(x16.size // 32):
+        x = x16[32 * b:32 * b + 32].astype(f32)
+        mx, sm = np.abs(x), x.copy()
+        for h in (16, 8, 4, 2):
+            mx[:h] = np.maximum(mx[:h], mx[h:2 * h])
+            sm[:h] = sm[:h] + sm[h:2 * h]
+        amax, s = max(mx[0], mx[1]), f32(sm[0] + sm[1])
+        dh = np.float16(f32(amax) / f32(127.0))
+        d = f32(dh)
+        inv = f32(1.0) / d if d != 0 else f32(0.0)
+        v = (x * inv).astype(np.float64)
+        q = np.clip(np.sign(v) * np.floor(np.abs(v) + 0.5), -127, 127).astype(np.int8)
+        out[b, 0:2] = np.frombuffer(dh.tobytes(), np.uint8)
+        out[b, 2:4] = np.frombuffer(np.float16(s).tobytes(), np.uint8)
+        out[b, 4:] = q.view(np.uint8)
+    return out
+
+
+def test_fused_f16_quantizer_two_restatements_agree(O):
+    """The C restatement (oracle) and an independent numpy one agree byte for byte; the reference's
+    own fused kernel is CUDA-only and racy, so this row is pinned by restatement."""
+    rng = np.random.default_rng(9)
+    rows = [(rng.standard_normal(256) * s).astype(np.float16) for s in (1e-3, 1.0, 40.0, 2000.0)]
+    rows.append(np.zeros(64, np.float16))
+    rows.append(rng.choice(np.array([-1000.0, 0.25, 3.0, -0.125, 1e-3], np.float16), size=256))
+    for x in rows:
+        assert np.array_equal(O.quantize_q8_1_fused_f16(x), _fused_f16_quantize_numpy(x))
+
+
+def test_fused_f16_gemm_oracle_transposes(O):
+    """qgo_gemm_q4_0_fp16_fused (weight-major) == the activation-major W4A8 oracle on the same bytes."""
+    rng = np.random.default_rng(4)
+    act = rng.standard_normal((5, 512)).astype(np.float16)
+    _, b = O.fill_uniform_step4(1, 24, 512)
+    wq = O.quantize(b, O.Q4_0)
+    out = O.gemm_q4_0_fp16_fused(wq, act)
+    assert np.array_equal(out, O.gemm_w4a8(O.quantize_q8_1_fused_f16(act), wq, O.Q4_0).T)

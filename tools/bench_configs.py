@@ -31,6 +31,26 @@ CONFIGS = [
 WT = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
 
 
+def graph_us(step, reps: int) -> float:
+    """Microseconds per replay of a hipGraph capturing step(stream)."""
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        step(ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    for _ in range(2):
+        g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
 def measure(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
     dev = torch.device("cuda", 0)
     wt = WT[wname]
@@ -59,28 +79,39 @@ def measure(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
                                   ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt, stream)
             assert st == 0, st
 
-    side = torch.cuda.Stream()
-    with torch.cuda.stream(side):
-        step(ctypes.c_void_p(side.cuda_stream))
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        step(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-    for _ in range(2):
-        g.replay()
+    us = graph_us(step, reps) / G
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / (reps * G)
     nbk = K // 32
     byts = N * nbk * bb + M * nbk * 36 + M * N * 4
     flops = 2.0 * M * N * K
     res = {"wtype": wname, "M": M, "N": N, "K": K, "algo": {1: "gemv", 2: "mfma", 3: "generic"}.get(algo, algo),
            "us_per_launch": round(us, 3), "gbps": round(byts / us / 1e3, 1), "frac_hbm": round(byts / us / 1e3 / PEAK, 4),
            "tflops": round(flops / us / 1e6, 3), "nmse_vs_fp32": nmse, "algorithmic_bytes": byts, "launches": G}
+    if M <= 8:
+        # FP32 activations: fused quantization (one launch) vs quantize + product (two launches)
+        a_c = a.contiguous()
+        ws = torch.empty((lib.qg_gemm_w4a8_f32_workspace_size(M, K),), dtype=torch.uint8, device=dev)
+        aq2 = torch.empty_like(aq)
+
+        def fused(stream):
+            for j in range(G):
+                st = lib.qg_gemm_w4a8_f32(ctypes.c_void_p(a_c.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                          ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt,
+                                          ctypes.c_void_p(ws.data_ptr()), ws.numel(), stream)
+                assert st == 0, st
+
+        def two_step(stream):
+            for j in range(G):
+                assert lib.qg_quantize_q8_1(ctypes.c_void_p(a_c.data_ptr()), ctypes.c_void_p(aq2.data_ptr()),
+                                            M * K, stream) == 0
+                assert lib.qg_gemm_w4a8(ctypes.c_void_p(aq2.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                        ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt, stream) == 0
+
+        fbytes = N * nbk * bb + M * K * 4 + M * N * 4
+        for name, fn in (("fused_f32", fused), ("quantize_then_gemm", two_step)):
+            uf = graph_us(fn, reps) / G
+            res[name] = {"us_per_product": round(uf, 3), "gbps": round(fbytes / uf / 1e3, 1),
+                         "frac_hbm": round(fbytes / uf / 1e3 / PEAK, 4)}
     if algo == 1:
         bout = torch.empty((G, M, N), dtype=torch.float32, device=dev)
         cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
