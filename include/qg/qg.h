@@ -71,6 +71,19 @@ int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, i
  * gemm_w8a8_reference (include/gemm_reference.h:233-267). Same as qg_gemm_w4a8(..., QG_TYPE_Q8_0). */
 int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream);
 
+/* ---- W4A16 / W8A16: FP32 activations, fp32 arithmetic -----------------
+ * C[M][N] = A_f32[M][K] . dequant(B)[N][K]^T, activation-major. Replaces gemm_w4a16_{naive,tiled}
+ * (include/gemm_cuda_naive.cuh:267-274, gemm_cuda_tiled.cuh:284-291) and gemm_w8a16_naive
+ * (gemm_cuda_naive.cuh:276-283); device twin of gemm_w4a16_reference (gemm_reference.h:73-112).
+ * Results agree with the reference to fp32 summation order (each block's products are summed,
+ * then scaled by d once). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0. */
+int qg_gemm_w4a16(const float* A, const void* B_q4_0, float* C, int M, int N, int K, qg_stream_t stream);
+int qg_gemm_w8a16(const float* A, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream);
+/* python/quant_gemm/csrc/gemm_ops.cu:431-466 gemm_q4_0_fp32_cuda(weight_q [N][K/32], activation
+ * [M][K], M, N, K) -> out[M][N]: the same product, weight-first argument order. */
+int qg_gemm_q4_0_fp32(const void* weight_q4_0, const float* activation, float* out, int M, int N, int K,
+                      qg_stream_t stream);
+
 /* Strided batch of independent products (e.g. the experts of an MoE layer, or several projections
  * sharing nothing): item i uses A + i*strideA, B + i*strideB (bytes) and C + i*strideC (floats).
  * One launch on the GEMV path (M <= 8), so the per-launch cost is paid once for the batch. */

@@ -95,6 +95,18 @@ int weight_major(int wtype, const void* W, const void* A, float* out, int M, int
     g.ldc_m = 1; g.ldc_n = N;
     return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)s);
 }
+int run_w16(int wtype, const float* A, const void* B, float* C, int M, int N, int K, hipStream_t st) {
+    if (M < 0 || N < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (M == 0 || N == 0) return QG_OK;
+    if (!A || !B || !C) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)A & 3) != 0 || ((uintptr_t)B & 1) != 0) return QG_ERR_ALIGN;
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    return hip_status(launch_w16(g, st));
+}
+
 size_t fused_workspace_bytes(int M, int K) { return M > 0 && K > 0 ? (size_t)M * (size_t)(K / 32) * 36 : 0; }
 
 // FP32 / FP16 activations (g.ain != AIN_Q8_1), dense rows of K elements. Small M: quantization
@@ -150,6 +162,19 @@ int run_fused(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st) {
 extern "C" {
 
 size_t qg_gemm_w4a8_f32_workspace_size(int M, int K) { return fused_workspace_bytes(M, K); }
+
+int qg_gemm_w4a16(const float* A, const void* B_q4_0, float* C, int M, int N, int K, qg_stream_t stream) {
+    return run_w16(QG_TYPE_Q4_0, A, B_q4_0, C, M, N, K, (hipStream_t)stream);
+}
+
+int qg_gemm_w8a16(const float* A, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream) {
+    return run_w16(QG_TYPE_Q8_0, A, B_q8_0, C, M, N, K, (hipStream_t)stream);
+}
+
+int qg_gemm_q4_0_fp32(const void* weight_q4_0, const float* activation, float* out, int M, int N, int K,
+                      qg_stream_t stream) {
+    return run_w16(QG_TYPE_Q4_0, activation, weight_q4_0, out, M, N, K, (hipStream_t)stream);
+}
 
 int qg_gemm_w4a8_f32(const float* X, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
                      size_t workspace_bytes, qg_stream_t stream) {

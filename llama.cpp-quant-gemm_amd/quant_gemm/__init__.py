@@ -263,6 +263,35 @@ def gemm_w8a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int
     return gemm_w4a8(activation_q, weight_q, M, N, K, wtype=Q8_0)
 
 
+# ---------------------------------------------------------------------------- W4A16 / W8A16
+def _gemm_w16(sym: str, wtype: int, activation: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int):
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(activation.is_cuda and activation.dtype == torch.float32, "Activation must be a CUDA float32 tensor")
+    _require(activation.numel() == M * K, f"Activation shape mismatch: expected {M * K} elements")
+    _check_blocks(weight_q, "Weight", N, K, BLOCK_BYTES[wtype])
+    a = activation.contiguous()
+    w = weight_q.contiguous()
+    out = torch.empty((M, N), dtype=torch.float32, device=w.device)
+    with torch.cuda.device(w.device):
+        _lib.check(getattr(_lib.load(), sym)(_ptr(a), _ptr(w), _ptr(out), M, N, K, _stream(w.device)), sym)
+    return out
+
+
+def gemm_w4a16(activation: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """C[M, N] = A_f32[M, K] . dequant(W_q4_0[N, K])^T (include/gemm_reference.h:73-112)."""
+    return _gemm_w16("qg_gemm_w4a16", Q4_0, activation, weight_q, M, N, K)
+
+
+def gemm_w8a16(activation: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """C[M, N] = A_f32[M, K] . dequant(W_q8_0[N, K])^T (include/gemm_cuda_naive.cuh:276-283)."""
+    return _gemm_w16("qg_gemm_w8a16", Q8_0, activation, weight_q, M, N, K)
+
+
+def gemm_q4_0_fp32(weight_q: torch.Tensor, activation: torch.Tensor, M: int, N: int, K: int) -> torch.Tensor:
+    """python/quant_gemm/csrc/gemm_ops.cu:431-466: weight_q [N, K/32, 18], activation [M, K] -> [M, N]."""
+    return _gemm_w16("qg_gemm_w4a16", Q4_0, activation, weight_q, M, N, K)
+
+
 def debug_sumi(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
                wtype: int = Q4_0, algo: int = ALGO_AUTO) -> torch.Tensor:
     """Per-block int32 dots [M, N, K/32] through the same decode path as ``algo``."""
@@ -292,5 +321,6 @@ __all__ = [
     "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
     "gemm_w4a8_batched", "debug_sumi", "select_algo", "version",
     "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused", "gemm_w8a8", "gemm_q8_0_q8_1",
+    "gemm_w4a16", "gemm_w8a16", "gemm_q4_0_fp32",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

@@ -37,6 +37,9 @@ SIGNATURES = {
     "qg_gemm_q4_0_fp16_fused": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_0_fp16_fused_ws": ([P, P, P, I, I, I, P, SZ, P], I),
     "qg_quantize_q8_1_f16_fused": ([P, P, I64, P], I),
+    "qg_gemm_w4a16": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_w8a16": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_q4_0_fp32": ([P, P, P, I, I, I, P], I),
     "qg_quantize_q8_1": ([P, P, I64, P], I),
     "qg_quantize_q4_0": ([P, P, I64, P], I),
     "qg_quantize": ([I, I, P, P, I64, P], I),

@@ -51,6 +51,7 @@ def lib() -> ctypes.CDLL:
         L.qgo_dequantize.argtypes = [I, P, P, I64]
         L.qgo_gemm_fp32.argtypes = [P, P, P, I, I, I]
         L.qgo_gemm_w4a16.argtypes = [P, P, P, I, I, I]
+        L.qgo_gemm_w8a16.argtypes = [P, P, P, I, I, I]
         L.qgo_gemm_w4a8.argtypes = [P, P, P, P, I, I, I, I]
         L.qgo_gemm_w4a8_mt.argtypes = [P, P, P, I, I, I, I, I]
         L.qgo_gemm_w8a8.argtypes = [P, P, P, I, I, I]
@@ -169,6 +170,22 @@ def gemm_w4a16(a: np.ndarray, b_q: np.ndarray) -> np.ndarray:
     c = np.empty((m, n), np.float32)
     lib().qgo_gemm_w4a16(_p(np.ascontiguousarray(a, np.float32)), _p(b_q), _p(c), m, n, k)
     return c
+
+
+def gemm_w8a16(a: np.ndarray, b_q: np.ndarray) -> np.ndarray:
+    m, k = a.shape
+    n = b_q.shape[0]
+    c = np.empty((m, n), np.float32)
+    lib().qgo_gemm_w8a16(_p(np.ascontiguousarray(a, np.float32)), _p(np.ascontiguousarray(b_q)), _p(c), m, n, k)
+    return c
+
+
+def w16_tol(a: np.ndarray, b_q: np.ndarray, t: int) -> np.ndarray:
+    """fp32 summation-order bound for W4A16/W8A16 outputs: 2 * (K + 2) * 2^-24 * sum_k |a_k w_k|
+    (K + 2: the K-term sum plus the per-element / per-block scaling roundings)."""
+    w = dequantize(b_q, t).astype(np.float64)
+    k = a.shape[1]
+    return 2.0 * (k + 2) * 2.0 ** -24 * (np.abs(a.astype(np.float64)) @ np.abs(w).T) + 1e-30
 
 
 def vec_dot_q4_0_q8_1(x_q4: np.ndarray, y_q8: np.ndarray) -> float:

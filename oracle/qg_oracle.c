@@ -21,6 +21,7 @@
  *   qgo_dequantize           include/quantize.h:84-102, 140-150, 198-210 + per-format formulas
  *   qgo_gemm_fp32            include/gemm_reference.h:38-58
  *   qgo_gemm_w4a16           include/gemm_reference.h:73-112
+ *   qgo_gemm_w8a16           include/gemm_cuda_naive.cuh:120-143 (no CPU reference exists for W8A16)
  *   qgo_gemm_w4a8            include/gemm_reference.h:175-222 (Q4_0) and, for Q4_1/Q5_0/Q5_1, the
  *                            same loop with the corrected block formulas of
  *                            kernels/gemm/gemm_quant_formats.cuh:105-267 (no /4, SURVEY.md §0.2;
@@ -384,6 +385,24 @@ void qgo_gemm_w4a16(const float* A, const void* Bv, float* C, int M, int N, int 
                     const int k_idx = b * QG_QK;
                     sum += A[(size_t)i * K + k_idx + k] * w0;
                     sum += A[(size_t)i * K + k_idx + k + QG_QK / 2] * w1;
+                }
+            }
+            C[(size_t)i * N + j] = sum;
+        }
+}
+
+/* include/gemm_cuda_naive.cuh:120-143 (gemm_w8a16_naive_kernel), the W8A16 sum order. */
+void qgo_gemm_w8a16(const float* A, const void* Bv, float* C, int M, int N, int K) {
+    const qg_block_q8_0* B = (const qg_block_q8_0*)Bv;
+    const int nb = K / QG_QK;
+    for (int i = 0; i < M; i++)
+        for (int j = 0; j < N; j++) {
+            float sum = 0.0f;
+            for (int b = 0; b < nb; b++) {
+                const float d = qgo_h2f(B[(size_t)j * nb + b].d);
+                for (int k = 0; k < QG_QK; k++) {
+                    const float w = B[(size_t)j * nb + b].qs[k] * d;
+                    sum += A[(size_t)i * K + b * QG_QK + k] * w;
                 }
             }
             C[(size_t)i * N + j] = sum;

@@ -9,6 +9,7 @@ never copied into this repo):
   quant_gemm/w4a8_q4_0_q8_1_n4096_k4096.json     -> W4A8 Q4_0 outputs  (json "reference", :77)
   quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json   -> W4A8 Q4_1 outputs  (:79)
   quantize/quantize_q8_1_k4096.json              -> Q8_1 bytes         (:66)
+  quant_gemm/w4a16_q4_0_fp32_n4096_k4096.json    -> W4A16 outputs (FP32 activations x Q4_0)
 
 The reference tree does not exist on the GPU box; the tests only read the .npz written here.
 Usage:  python tests/golden/make_golden.py [--ref /root/reference]
@@ -56,6 +57,14 @@ def w4a8_case(run, m, n, k, wtype, seed=42):
                 c_fp32=O.gemm_fp32(a, b))
 
 
+def w4a16_case(run, m, n, k, seed=42):
+    import torch
+    a, b = O.fill_uniform_step4(m, n, k, seed)
+    b_q = O.quantize(b, O.Q4_0)
+    c_ref = run(torch.from_numpy(a), as_block_objects(b_q)).numpy().astype(np.float32)
+    return dict(m=np.int32(m), n=np.int32(n), k=np.int32(k), seed=np.int32(seed), a=a, b_q=b_q, c_ref=c_ref)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -64,6 +73,7 @@ def main() -> None:
     run_q4_0 = load_reference_fn(args.ref, "quant_gemm/w4a8_q4_0_q8_1_n4096_k4096.json")
     run_q4_1 = load_reference_fn(args.ref, "quant_gemm/w4_1a8_q4_1_q8_1_n4096_k4096.json")
     quant_q8_1 = load_reference_fn(args.ref, "quantize/quantize_q8_1_k4096.json", "quantize_block_q8_1")
+    run_w4a16 = load_reference_fn(args.ref, "quant_gemm/w4a16_q4_0_fp32_n4096_k4096.json")
 
     cases = {
         # BASELINE.json configs[0]: the plumbing config, in full
@@ -73,6 +83,8 @@ def main() -> None:
         "w4a8_q4_1_m2n8k128": w4a8_case(run_q4_1, 2, 8, 128, O.Q4_1),
         "w4a8_q4_1_m1n16k256": w4a8_case(run_q4_1, 1, 16, 256, O.Q4_1, seed=3),
     }
+    cases["w4a16_q4_0_m2n16k256"] = w4a16_case(run_w4a16, 2, 16, 256)
+    cases["w4a16_q4_0_m3n8k96"] = w4a16_case(run_w4a16, 3, 8, 96, seed=5)
     for name, d in cases.items():
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
         print(f"{name}: C[0,:4]={d['c_ref'].ravel()[:4]}")

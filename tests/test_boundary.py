@@ -88,6 +88,12 @@ def test_validation_codes_without_launch(lib):
     assert so.qg_quantize(9, 0, fake, P(4098), 32, None) == -4               # Q8_1 blocks need 4-B alignment
     assert so.qg_quantize(9, 0, None, None, 0, None) == 0
     assert so.qg_dequantize(5, fake, fake, 32, None) == -3
+    # W4A16 / W8A16
+    assert so.qg_gemm_w4a16(fake, fake, fake, 1, 1, 48, None) == -2
+    assert so.qg_gemm_w4a16(P(4098), fake, fake, 1, 1, 64, None) == -4           # floats misaligned
+    assert so.qg_gemm_w8a16(fake, P(4097), fake, 1, 1, 64, None) == -4
+    assert so.qg_gemm_q4_0_fp32(fake, None, fake, 1, 1, 64, None) == -1
+    assert so.qg_gemm_w4a16(None, None, None, 0, 3, 64, None) == 0
     # fused activation quantization
     assert so.qg_gemm_w4a8_f32_workspace_size(3, 4096) == 3 * 128 * 36
     assert so.qg_gemm_w4a8_f32_workspace_size(0, 4096) == 0
