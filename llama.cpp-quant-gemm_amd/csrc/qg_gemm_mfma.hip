@@ -3,31 +3,42 @@
 //
 // Tile configuration from the sweeps in tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
 // mmq_probe_smallm.txt; cold weights, one MI355X):
-//  * M <= 64: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
+//  * M <= 32: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
 //    >= 256 workgroups (one per CU; fewer re-reads of the activations), else 16
 //    (M=32, N=4096: 32 rows x 2 token tiles = 256 WGs; M=8, N=4096: 16 rows = 256 WGs)
-//  * M  > 64: 32 rows x 64 tokens, 4 waves (more reuse of each staged stage per MFMA)
+//  * M  > 32: 32 rows x 32 tokens; 8 waves splitting K while that grid has <= 512 workgroups, else
+//    4 (profiles/r01_tuning/mmq_probe_p4.txt: M=64 10.3 us, M=128 17.5 us, M=512 58 us; the
+//    former 32 rows x 64 tokens took 13.6 / 21.7 / 76.6 us)
 #include "qg_mmq_kernel.hpp"
 
 namespace qg {
 
 namespace {
-template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) { return mmq_shape_ok<F, BN, TT, W>(g); }
+// 16-B weight DMA pieces when K % 256 == 0 and B is 16-B aligned, else 4-B pieces.
+template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
+    return mmq_shape_ok<F, BN, TT, W, true>(g) || mmq_shape_ok<F, BN, TT, W, false>(g);
+}
+
+template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
+    return g.sumi ? mmq_launch<F, BN, TT, W, true, P16>(g, st) : mmq_launch<F, BN, TT, W, false, P16>(g, st);
+}
 
 template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hipStream_t st) {
-    return g.sumi ? mmq_launch<F, BN, TT, W, true>(g, st) : mmq_launch<F, BN, TT, W, false>(g, st);
+    return mmq_shape_ok<F, BN, TT, W, true>(g) ? run_p<F, BN, TT, W, true>(g, st) : run_p<F, BN, TT, W, false>(g, st);
 }
 
 inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
 
+inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 512; }
+
 template <int F> bool ok_f(const GemmArgs& g) {
-    if (g.M <= 64) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);
-    return ok_cfg<F, 32, 4, 4>(g);
+    if (g.M <= 32) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);
+    return few_tiles(g) ? ok_cfg<F, 32, 2, 8>(g) : ok_cfg<F, 32, 2, 4>(g);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
-    if (g.M <= 64) return wide_rows(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 16, 1, 8>(g, st);
-    return run_cfg<F, 32, 4, 4>(g, st);
+    if (g.M <= 32) return wide_rows(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 16, 1, 8>(g, st);
+    return few_tiles(g) ? run_cfg<F, 32, 2, 8>(g, st) : run_cfg<F, 32, 2, 4>(g, st);
 }
 }  // namespace
 

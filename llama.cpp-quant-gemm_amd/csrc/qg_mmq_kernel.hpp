@@ -14,22 +14,23 @@
 // Operand k-order: lane (r = lane&15, q = lane>>4) supplies, for its weight row / token r, the 8
 // bytes of k-slot q: elements 4q..4q+3 and 16+4q..16+4q+3 of the block. For the weights that is qs
 // dword q split into low / high nibbles (+ the qh bits for Q5_x), for Q8_0 its signed qs dwords q and
-// 4+q; for the activations qs dwords q and 4+q. Q8_0 (W8A8) runs the Q4_0 epilogue with no s_a term. A and B use the same slot -> element map and the integer sum is order-free.
+// 4+q; for the activations qs dwords q and 4+q. A and B use the same slot -> element map and the
+// integer sum is order-free. Q8_0 (W8A8) runs the Q4_0 epilogue with no s_a term.
 // C layout (gfx950, dtype-independent): lane holds column m = lane&15, rows n = 4q + e (e < 4), so
-// the token's scales are per-lane scalars and the 4 row scales come from a small LDS table.
+// the token's scales are per-lane scalars and the 4 row scales are 4 fp16 reads of the staged rows.
 //
 // Tiling: a workgroup owns BN weight rows x 16*TT tokens and ALL of K; its W waves
-// split K into 128-element stages (4 blocks), wave w taking stages w, w+W, ... With BN = 16,
-// TT = 2 the M = 32, N = 4096 prefill is 256 workgroups, one per CU. Each wave streams its stages
+// split K into 128-element stages (4 blocks), wave w taking stages w, w+W, ... With BN = 32,
+// TT = 1 the M = 32, N = 4096 prefill is 256 workgroups, one per CU. Each wave streams its stages
 // with LDS-DMA (global_load_lds: no VGPR staging, lane-linear LDS images [row][4 blocks] and
 // [token][144 B]) into two wave-private LDS buffers, the next stage in flight while the current one
 // computes (counted vmcnt). No workgroup barrier in the main loop; the W partial tiles are summed
 // in fixed wave order through LDS at the end.
 //
-// MFMA results are read only after the next block's MFMAs have issued (software pipeline inside a
-// stage) or behind an explicit wait (the stage's last block): reading them with only the wait
-// states hipcc inserts for this instruction on gfx950 gave wrong sums on the GPU
-// (tools/mmq_debug.hip).
+// A stage runs in three phases (all LDS reads, all MFMAs, all epilogues) so that each phase's
+// latencies overlap; MFMA results are read behind an explicit wait: reading them with only the wait
+// states hipcc inserts for this instruction on gfx950 gave wrong sums (tools/mmq_debug.hip). Only
+// LDS reads in the main loop: an LDS write there makes hipcc wait for every DMA in flight.
 #pragma once
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
@@ -69,36 +70,43 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
     else __builtin_amdgcn_global_load_lds(gp, lp, 4, 0, 0);
 }
 
-template <int F, int BN, int TT, int W> struct mmq_geom {
+// P16: weights DMA'd in 16-B pieces (16-B aligned B and rows; else 4-B pieces). A
+// stage's row segment (RSB = 4 * BB bytes) then starts 16-B aligned or 8 bytes past (RSB % 16 == 8
+// for Q4_0 / Q5_0 / Q8_0, alternating with the stage parity): each row image is a 16-B aligned
+// window of RIMG bytes and the data sits SHIFT(h) = (h * RSB) % 16 bytes into it. With K % 256 == 0
+// the stage count is even, so the last stage is an odd one (shift 8) and no window reaches past
+// the end of the weight rows.
+template <int F, int BN, int TT, int W, bool P16 = false> struct mmq_geom {
     using T = wfmt<F>;
     static constexpr int RSB = MMQ_SB * T::BB;                // weight bytes per row per stage
-    static constexpr int WPS = RSB % 16 == 0 ? 16 : 4;          // weight DMA piece (bytes)
-    static constexpr int WPC = BN * RSB / WPS;                 // weight pieces per stage
+    static constexpr int WPS = P16 ? 16 : 4;                   // weight DMA piece (bytes)
+    static constexpr int RIMG = P16 && RSB % 16 != 0 ? RSB + 8 : RSB;  // row image bytes
+    static constexpr int PPR = RIMG / WPS;                     // pieces per row image
+    static constexpr int WPC = BN * PPR;                       // weight pieces per stage
     static constexpr int NWI = (WPC + 63) / 64;                // weight DMA instructions per stage
     static constexpr int NTOK = 16 * TT;
     static constexpr int APC = NTOK * 9;                       // activation 16-B pieces per stage
     static constexpr int NAI = (APC + 63) / 64;                // activation DMA instructions per stage
     static constexpr int NI = NWI + NAI;
     static constexpr int RT = BN / 16;                         // row tiles
-    static constexpr int NMW = T::MOFF >= 0 ? 2 : 1;           // weight scale tables: d (and m)
     // LDS buffer layout (bytes). Every DMA instruction runs on all 64 lanes (see issue()), so the
     // weight and activation images are padded to whole instructions.
     static constexpr int OFF_A = NWI * 64 * WPS;
-    static constexpr int OFF_WT = OFF_A + NAI * 64 * 16;
-    static constexpr int OFF_AT = OFF_WT + MMQ_SB * NMW * BN * 4;
-    static constexpr int BUF = OFF_AT + MMQ_SB * NTOK * 16;
+    static constexpr int BUF = OFF_A + NAI * 64 * 16;
     static constexpr int NACC = RT * TT * 4;                   // accumulators per lane
     // wave buffers; the end-of-kernel partial tiles reuse them (after a barrier)
     static constexpr size_t LDS = (size_t)W * (2 * BUF > NACC * 256 ? 2 * BUF : NACC * 256);
     static_assert(LDS <= 160 * 1024, "LDS per workgroup");
-    static_assert(OFF_WT % 16 == 0 && OFF_AT % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
+    static_assert(OFF_A % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
+    static_assert(RSB % 8 == 0, "stage segments are 8-B multiples");
+    __host__ __device__ static constexpr int shift(int h) { return P16 ? (h * RSB) & 15 : 0; }
 };
 
-template <int F, int BN, int TT, int W, bool SUMI>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n) {
-    using G = mmq_geom<F, BN, TT, W>;
+    using G = mmq_geom<F, BN, TT, W, P16>;
     using T = wfmt<F>;
     static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -125,8 +133,8 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #pragma unroll
     for (int i = 0; i < G::NWI; ++i) {
         const int p = min(64 * i + lane, G::WPC - 1);
-        const int row = p / (G::RSB / G::WPS);
-        woff[i] = (int)((long)min(n0 + row, N - 1) * RB) + (p - row * (G::RSB / G::WPS)) * G::WPS;
+        const int row = p / G::PPR;
+        woff[i] = (int)((long)min(n0 + row, N - 1) * RB) + (p - row * G::PPR) * G::WPS;
     }
 #pragma unroll
     for (int i = 0; i < G::NAI; ++i) {
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     // per-lane M0 base, read back with v_readfirstlane — wrong destinations for half the wave
     // (found by tools/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
-        const uint8_t* wsrc = B + (long)h * G::RSB;
+        const uint8_t* wsrc = B + (long)h * G::RSB - G::shift(h);
         const uint8_t* asrc = A + (long)h * 144;
 #pragma unroll
         for (int i = 0; i < G::NWI; ++i) glds<G::WPS>(wsrc + woff[i], buf + 64 * i * G::WPS);
@@ -152,34 +160,18 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     for (int i = 0; i < G::NACC; ++i) acc[i] = 0.0f;
     const v4i bias = {MMQ_BIAS, MMQ_BIAS, MMQ_BIAS, MMQ_BIAS};
 
-    // Scale tables of a staged stage, converted once per wave: weight d (and m) as f32
-    // [block][d|m][row]; activation {d_a, -d_a * 1.5*2^23, c * s_a} as f32x4 [block][token] with
-    // c = 8 (Q4_0), 16 (Q5_0) or 1 (Q4_1 / Q5_1: m_w * s_a).
-    auto prep = [&](uint8_t* buf) {
-        float* wt = reinterpret_cast<float*>(buf + G::OFF_WT);
-        float4* at = reinterpret_cast<float4*>(buf + G::OFF_AT);
-#pragma unroll
-        for (int j = lane; j < MMQ_SB * BN; j += 64) {
-            const int b = j / BN, row = j - b * BN;
-            const uint8_t* blk = buf + row * G::RSB + b * T::BB;
-            wt[b * G::NMW * BN + row] = h2f(*reinterpret_cast<const uint16_t*>(blk));
-            if constexpr (T::MOFF >= 0) wt[b * G::NMW * BN + BN + row] = h2f(*reinterpret_cast<const uint16_t*>(blk + T::MOFF));
-        }
-#pragma unroll
-        for (int j = lane; j < MMQ_SB * G::NTOK; j += 64) {
-            const int b = j / G::NTOK, tk = j - b * G::NTOK;
-            const uint32_t dsh = *reinterpret_cast<const uint32_t*>(buf + G::OFF_A + tk * 144 + b * Q8_1_BYTES);
-            const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
-            constexpr float cs = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : 1.0f;
-            at[j] = make_float4(da, -(da * MMQ_BIAS_F), cs * sa, 0.0f);
-        }
-    };
-
+    // Block scales straight from the staged images, per lane: d (and m) of the 4 weight rows
+    // 16 i + 4 q + e it accumulates, {d_a, -d_a * 1.5*2^23, c * s_a} of its token 16 t + r16 with
+    // c = 8 (Q4_0), 16 (Q5_0), 0 (Q8_0) or 1 (Q4_1 / Q5_1: m_w * s_a). Only LDS reads in the
+    // main loop: an LDS write there makes hipcc wait for every DMA in flight (vmcnt(0)), which
+    // serialised the double buffer.
+    constexpr float CS = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : 1.0f;
     struct blk_t {
         v4i c[G::RT][TT];
         float4 dw[G::RT], mw[G::RT];
         float4 as[TT];  // {d_a, -d_a * bias, c * s_a, -}
     };
+    auto h16 = [](const uint8_t* p) { return h2f(*reinterpret_cast<const uint16_t*>(p)); };
     auto epilogue = [&](const blk_t& p, int h, int b) {
 #pragma unroll
         for (int t = 0; t < TT; ++t)
@@ -210,19 +202,20 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
             }
     };
 
-    // the 4 blocks of one staged stage: fragments, MFMAs, epilogues one block behind
-    auto compute = [&](uint8_t* buf, int h) {
-        const float* wt = reinterpret_cast<const float*>(buf + G::OFF_WT);
-        const float4* at = reinterpret_cast<const float4*>(buf + G::OFF_AT);
-        blk_t prev;
+    // The 4 blocks of one staged stage in three phases, so each phase's latencies overlap: every
+    // LDS read of the stage (operand fragments and block scales) in flight together, then the
+    // 4 x RT x TT MFMAs back to back, then the VALU epilogues (block b's results are read behind
+    // the later blocks' MFMAs and epilogues, plus an explicit wait for the matrix pipe: reading
+    // them with only the wait states hipcc inserts gave wrong sums, tools/mmq_debug.hip).
+    auto compute = [&](uint8_t* buf, int h, int sh) {
+        blk_t blk[MMQ_SB];
+        long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
         static_for<MMQ_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
             constexpr int o = b * T::BB;
-            blk_t cur;
-            long afrag[G::RT], bfrag[TT];
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
-                const uint8_t* wr = buf + (16 * i + r16) * G::RSB;
+                const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
                 uint32_t lo, hi;
                 if constexpr (T::Q8) {  // signed bytes, elements 4q.. and 16+4q..
                     lo = lds32<o + T::QS>(wr + 4 * q);
@@ -237,33 +230,38 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
                     lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
                     hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
                 }
-                afrag[i] = (long)(((unsigned long)hi << 32) | lo);
-                cur.dw[i] = *reinterpret_cast<const float4*>(wt + b * G::NMW * BN + 16 * i + 4 * q);
-                if constexpr (T::MOFF >= 0) cur.mw[i] = *reinterpret_cast<const float4*>(wt + b * G::NMW * BN + BN + 16 * i + 4 * q);
-                else cur.mw[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
+                const uint8_t* sr = buf + (16 * i + 4 * q) * G::RIMG + sh + o;  // rows 16 i + 4 q + e
+                blk[b].dw[i] = make_float4(h16(sr), h16(sr + G::RIMG), h16(sr + 2 * G::RIMG), h16(sr + 3 * G::RIMG));
+                if constexpr (T::MOFF >= 0)
+                    blk[b].mw[i] = make_float4(h16(sr + T::MOFF), h16(sr + G::RIMG + T::MOFF),
+                                               h16(sr + 2 * G::RIMG + T::MOFF), h16(sr + 3 * G::RIMG + T::MOFF));
+                else blk[b].mw[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * 144 + b * Q8_1_BYTES;
                 const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
                 const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
-                bfrag[t] = (long)(((unsigned long)qa1 << 32) | qa0);
-                cur.as[t] = at[b * G::NTOK + 16 * t + r16];
+                bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
+                const uint32_t dsh = *reinterpret_cast<const uint32_t*>(ar);
+                const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
+                blk[b].as[t] = make_float4(da, -(da * MMQ_BIAS_F), CS * sa, 0.0f);
             }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
                 for (int i = 0; i < G::RT; ++i)
-                    cur.c[i][t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(afrag[i], bfrag[t], bias, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (b > 0) epilogue(prev, h, b - 1);
-            __builtin_amdgcn_sched_barrier(0);
-            prev = cur;
+                    blk[b].c[i][t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(afrag[b][i], bfrag[b][t], bias, 0, 0, 0);
         });
-        // the stage's last block has no MFMA behind it: wait out the matrix pipe explicitly
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        epilogue(prev, h, MMQ_SB - 1);
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -280,8 +278,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #ifdef QG_MMQ_STAMPS
         if (h == wave) MMQ_STAMP(1);
 #endif
-        prep(cur);
-        compute(cur, h);
+        compute(cur, h, G::shift(h));
 #ifdef QG_MMQ_STAMPS
         if (h == wave) MMQ_STAMP(2);
 #endif
@@ -316,23 +313,25 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 }
 
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
-// rows and stages aligned to the DMA piece, 32-bit byte offsets.
-template <int F, int BN, int TT, int W>
+// rows and stages aligned to the DMA piece, 32-bit byte offsets. P16 additionally: a 16-B aligned B
+// and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_geom).
+template <int F, int BN, int TT, int W, bool P16>
 inline bool mmq_shape_ok(const GemmArgs& g) {
-    using G = mmq_geom<F, BN, TT, W>;
+    using G = mmq_geom<F, BN, TT, W, P16>;
     if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_SB) != 0) return false;
     const long RB = (long)(g.K / QK) * wfmt<F>::BB, AB = (long)(g.K / QK) * Q8_1_BYTES;
     if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
-    if (((uintptr_t)g.B % (G::WPS == 16 ? 16 : 4)) != 0 || RB % G::WPS != 0) return false;
+    if (P16 && G::RSB % 16 != 0 && g.K % 256 != 0) return false;
+    if (((uintptr_t)g.B % G::WPS) != 0 || RB % G::WPS != 0) return false;
     if (RB * g.N >= (1L << 31) || AB * g.M >= (1L << 31)) return false;
     return true;
 }
 
-template <int F, int BN, int TT, int W, bool SUMI>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
-    using G = mmq_geom<F, BN, TT, W>;
+    using G = mmq_geom<F, BN, TT, W, P16>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16>;
     if (G::LDS > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {

@@ -125,11 +125,27 @@ def test_mfma_matches_oracle(O, qg, t, m):
     assert_close_to_oracle(O, c, aq, bq, t)
 
 
-@pytest.mark.parametrize("m,n,k", [(12, 33, 512), (64, 4096, 256), (32, 65, 8192)])
-def test_mfma_ragged(O, qg, m, n, k):
-    _, _, aq, bq = make_case(O, m, n, k, 2)
-    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, 2, algo=2))
-    assert_close_to_oracle(O, c, aq, bq, 2)
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("m,n,k", [(12, 33, 512), (64, 4096, 256), (32, 65, 8192), (10, 40, 384), (33, 20, 640)])
+def test_mfma_ragged(O, qg, t, m, n, k):
+    """Ragged tiles; K % 256 == 128 takes the 4-byte weight-DMA variant, K % 256 == 0 the 16-byte one."""
+    _, _, aq, bq = make_case(O, m, n, k, t)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=2))
+    assert_close_to_oracle(O, c, aq, bq, t)
+
+
+@pytest.mark.parametrize("t", WTYPES)
+def test_mfma_weights_4byte_aligned(O, qg, t):
+    """Weights only 4-B aligned: the 16-byte DMA variant is not legal, the 4-byte one runs."""
+    import torch
+    m, n, k = 20, 48, 1024
+    _, _, aq, bq = make_case(O, m, n, k, t)
+    raw = torch.zeros(bq.size + 4, dtype=torch.uint8, device="cuda")
+    raw[4:] = dev(bq.ravel())
+    w = raw[4:]
+    assert w.data_ptr() % 16 == 4
+    c = host(qg.gemm_w4a8(dev(aq), w, m, n, k, t, algo=2))
+    assert_close_to_oracle(O, c, aq, bq, t)
 
 
 @pytest.mark.parametrize("m,t", [(1, 2), (3, 6), (12, 2)])

@@ -35,15 +35,15 @@ static void check(int M, int N, int K) {
     CK(hipMemcpy(da, ha.data(), ha.size(), hipMemcpyHostToDevice)); CK(hipMemcpy(dw, hw.data(), hw.size(), hipMemcpyHostToDevice));
     CK(hipMemset(ds, 0, want.size() * 4));
     GemmArgs g; g.A = da; g.B = dw; g.C = dc; g.sumi = ds; g.M = M; g.N = N; g.K = K; g.wtype = F; g.ldc_m = N; g.ldc_n = 1;
-    if (!mmq_shape_ok<F, BN, TT, W>(g)) { printf("shape rejected\n"); return; }
-    CK((mmq_launch<F, BN, TT, W, true>(g, 0)));
+    if (!mmq_shape_ok<F, BN, TT, W, false>(g)) { printf("shape rejected\n"); return; }
+    CK((mmq_launch<F, BN, TT, W, true, false>(g, 0)));
     CK(hipDeviceSynchronize());
     std::vector<int> got(want.size());
     CK(hipMemcpy(got.data(), ds, got.size() * 4, hipMemcpyDeviceToHost));
     int bad = 0;
     for (size_t i = 0; i < want.size(); ++i) bad += got[i] != want[i];
     g.sumi = nullptr;
-    CK((mmq_launch<F, BN, TT, W, false>(g, 0)));
+    CK((mmq_launch<F, BN, TT, W, false, false>(g, 0)));
     CK(hipDeviceSynchronize());
     std::vector<float> c(M * N);
     CK(hipMemcpy(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));

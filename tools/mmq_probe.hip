@@ -22,7 +22,7 @@
 using namespace qg;
 
 static uint16_t f2h(float f) { _Float16 h = (_Float16)f; uint16_t b; memcpy(&b, &h, 2); return b; }
-static int block_bytes(int f) { return f == FMT_Q4_0 ? 18 : f == FMT_Q4_1 ? 20 : f == FMT_Q5_0 ? 22 : 24; }
+static int block_bytes(int f) { return f == FMT_Q4_0 ? 18 : f == FMT_Q4_1 ? 20 : f == FMT_Q5_0 ? 22 : f == FMT_Q8_0 ? 34 : 24; }
 
 typedef std::function<hipError_t(const GemmArgs&, hipStream_t)> LaunchFn;
 struct Variant { std::string name; LaunchFn fn; };
@@ -31,9 +31,9 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     struct S { int F, M, N, K; };
-    const S shapes[] = {{FMT_Q4_0, 2, 4096, 4096}, {FMT_Q4_0, 3, 4096, 4096}, {FMT_Q4_0, 4, 4096, 4096},
-                        {FMT_Q4_0, 6, 4096, 4096}, {FMT_Q4_0, 8, 4096, 4096}, {FMT_Q5_1, 4, 4096, 4096},
-                        {FMT_Q5_1, 8, 4096, 4096}, {FMT_Q4_0, 8, 4096, 14336}, {FMT_Q4_0, 8, 32000, 4096}};
+    const S shapes[] = {{FMT_Q4_0, 32, 4096, 4096}, {FMT_Q4_0, 8, 4096, 4096}, {FMT_Q4_0, 64, 4096, 4096},
+                        {FMT_Q4_0, 128, 4096, 4096}, {FMT_Q4_0, 512, 4096, 4096}, {FMT_Q5_1, 32, 4096, 4096},
+                        {FMT_Q8_0, 32, 4096, 4096}, {FMT_Q4_0, 16, 4096, 14336}};
     for (const S& s : shapes) {
         const int nb = s.K / 32, bb = block_bytes(s.F);
         const long wbytes = (long)s.N * nb * bb;
@@ -44,6 +44,7 @@ int main() {
             for (int j = 0; j < bb; ++j) hw[b * bb + j] = rand() & 0xFF;
             uint16_t d = f2h(0.01f + 0.09f * (float)rand() / (float)RAND_MAX);
             memcpy(&hw[b * bb], &d, 2);
+            if (s.F == FMT_Q8_0) for (int j = 2; j < bb; ++j) hw[b * bb + j] = (uint8_t)(rand() % 255 - 127);
             if (s.F == FMT_Q4_1 || s.F == FMT_Q5_1) { uint16_t m = f2h(-0.5f * (float)rand() / (float)RAND_MAX); memcpy(&hw[b * bb + 2], &m, 2); }
         }
         for (long b = 0; b < (long)s.M * nb; ++b) {
@@ -59,13 +60,18 @@ int main() {
         std::vector<Variant> vs;
         vs.push_back({"gemv (C-ABI algo 1)", [](const GemmArgs& g, hipStream_t st) { return qg_gemm_w4a8_ex(g.A, g.B, g.C, g.M, g.N, g.K, g.wtype, 1, (qg_stream_t)st) == 0 ? hipSuccess : hipErrorUnknown; }});
         vs.push_back({"product (C-ABI algo 2)", [](const GemmArgs& g, hipStream_t st) { return qg_gemm_w4a8_ex(g.A, g.B, g.C, g.M, g.N, g.K, g.wtype, 2, (qg_stream_t)st) == 0 ? hipSuccess : hipErrorUnknown; }});
-#define V(BN, TT, W, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        switch (g.wtype) { case FMT_Q4_0: return mmq_shape_ok<FMT_Q4_0, BN, TT, W>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false>(g, st) : hipErrorInvalidValue; \
-                           default: return mmq_shape_ok<FMT_Q5_1, BN, TT, W>(g) ? mmq_launch<FMT_Q5_1, BN, TT, W, false>(g, st) : hipErrorInvalidValue; } }});
-        V(16, 1, 8, "mmq bn16 tt1 w8")
-        V(16, 2, 8, "mmq bn16 tt2 w8")
-        V(32, 1, 8, "mmq bn32 tt1 w8")
-        V(32, 4, 4, "mmq bn32 tt4 w4")
+        // Q4_0 configurations only (other formats: the product dispatch above)
+#define V(BN, TT, W, P16, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, P16>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, st) : hipErrorInvalidValue; }});
+        V(32, 1, 8, true, "mmq bn32 tt1 w8 p16")
+        V(16, 1, 8, true, "mmq bn16 tt1 w8 p16")
+        V(32, 2, 4, true, "mmq bn32 tt2 w4 p16")
+        V(32, 2, 8, true, "mmq bn32 tt2 w8 p16")
+        V(16, 2, 8, true, "mmq bn16 tt2 w8 p16")
+        V(16, 4, 4, true, "mmq bn16 tt4 w4 p16")
+        V(48, 2, 4, true, "mmq bn48 tt2 w4 p16")
+        V(32, 3, 4, true, "mmq bn32 tt3 w4 p16")
+        V(32, 2, 2, true, "mmq bn32 tt2 w2 p16")
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
                                  g.wtype = s.F; g.ldc_m = s.N; g.ldc_n = 1; return g; };

@@ -10,7 +10,7 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 using namespace qg;
 static uint16_t f2h(float f) { _Float16 h = (_Float16)f; uint16_t b; memcpy(&b, &h, 2); return b; }
-template <int BN, int TT, int W>
+template <int BN, int TT, int W, bool P16>
 static void run(const char* name, int M, int N, int K) {
     const int nb = K / 32;
     const long wbytes = (long)N * nb * 18;
@@ -28,7 +28,7 @@ static void run(const char* name, int M, int N, int K) {
     const int L = 100;
     for (int rep = 0; rep < 2; ++rep) {
         CK(hipEventRecord(e0, 0));
-        for (int i = 0; i < L; ++i) { g.B = w[i % R]; CK((mmq_launch<FMT_Q4_0, BN, TT, W, false>(g, 0))); }
+        for (int i = 0; i < L; ++i) { g.B = w[i % R]; CK((mmq_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, 0))); }
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         const int nwg = ((N + BN - 1) / BN) * ((M + 16 * TT - 1) / (16 * TT)), nw = nwg * W;
@@ -54,8 +54,8 @@ static void run(const char* name, int M, int N, int K) {
     CK(hipFree(a)); CK(hipFree(c));
 }
 int main() {
-    run<16, 2, 8>("bn16 tt2 w8", 32, 4096, 4096);
-    run<32, 1, 8>("bn32 tt1 w8", 32, 4096, 4096);
-    run<16, 2, 4>("bn16 tt2 w4", 32, 4096, 4096);
+    run<32, 1, 8, false>("bn32 tt1 w8 p4", 32, 4096, 4096);
+    run<32, 1, 8, true>("bn32 tt1 w8 p16", 32, 4096, 4096);
+    run<32, 4, 4, true>("bn32 tt4 w4 p16", 512, 4096, 4096);
     return 0;
 }
