@@ -157,6 +157,52 @@ typedef struct {
 
 int qg_gemm_w4a8_from_view(const qg_tensor_view* activation, const qg_tensor_view* weights, qg_tensor_view* output,
                            const char* kernel_type, qg_stream_t stream);
+/* gemm_w4a16_from_ggml (llama_adapter.h:78-90): activation F32 [K, M], weights Q4_0 or Q8_0
+ * [K, N], output F32 [N, M]; kernel_type NULL / "naive" / "tiled" / "auto". */
+int qg_gemm_w4a16_from_view(const qg_tensor_view* activation, const qg_tensor_view* weights, qg_tensor_view* output,
+                            const char* kernel_type, qg_stream_t stream);
+/* gemm_fp32_from_ggml (llama_adapter.h:92-103): all three F32. */
+int qg_gemm_fp32_from_view(const qg_tensor_view* activation, const qg_tensor_view* weights, qg_tensor_view* output,
+                           const char* kernel_type, qg_stream_t stream);
+/* validate_tensor_types (llama_adapter.h:110-117): 1 if all three types match, else 0. */
+int qg_validate_view_types(const qg_tensor_view* activation, const qg_tensor_view* weights,
+                           const qg_tensor_view* output, int expected_activation_type, int expected_weight_type,
+                           int expected_output_type);
+
+/* ---- FP32 GEMM C[M][N] = A[M][K] . B[N][K]^T: the unquantized baseline the NMSE is quoted against
+ * (gemm_fp32_naive, include/gemm_cuda_naive.cuh:258-265; gemm_fp32_reference,
+ * gemm_reference.h:38-58). Any K >= 0, 4-B aligned floats. */
+int qg_gemm_fp32(const float* A, const float* B, float* C, int M, int N, int K, qg_stream_t stream);
+
+/* ---- GGUF weight files -------------------------------------------------
+ * A read-only mapping of a GGUF v2/v3 file: metadata and tensor directory; Q4_0/Q4_1/Q5_0/Q5_1/
+ * Q8_0/Q8_1/F16/F32 tensor data are the same bytes the kernels take. Host-side only, except
+ * qg_gguf_upload_tensor (a stream-ordered copy, then a stream sync). Every length and offset is
+ * checked against the file size; an unreadable or inconsistent file is QG_ERR_INVALID_ARG.
+ * Tensor dims follow ggml: ne[0] = K (contiguous), ne[1] = rows; unused dims are 1. */
+typedef struct qg_gguf qg_gguf;
+int qg_gguf_open(const char* path, qg_gguf** out);
+void qg_gguf_close(qg_gguf* file);
+int qg_gguf_version(const qg_gguf* file);
+int64_t qg_gguf_alignment(const qg_gguf* file);
+int64_t qg_gguf_tensor_count(const qg_gguf* file);
+int64_t qg_gguf_find_tensor(const qg_gguf* file, const char* name);   /* -1 if absent */
+int qg_gguf_tensor_info(const qg_gguf* file, int64_t index, const char** name, int* type, int* n_dims,
+                        int64_t ne[4], uint64_t* nbytes);               /* nbytes 0: type not supported */
+const void* qg_gguf_tensor_data(const qg_gguf* file, int64_t index);   /* host pointer into the mapping */
+int qg_gguf_upload_tensor(const qg_gguf* file, int64_t index, void* device_dst, size_t dst_bytes,
+                          qg_stream_t stream);
+/* a ggml-ordered view of the tensor's bytes at device_data, for the *_from_view entry points */
+int qg_gguf_tensor_view(const qg_gguf* file, int64_t index, void* device_data, qg_tensor_view* out);
+int64_t qg_gguf_kv_count(const qg_gguf* file);
+int64_t qg_gguf_find_kv(const qg_gguf* file, const char* key);         /* -1 if absent */
+/* GGUF value types: 0 u8, 1 i8, 2 u16, 3 i16, 4 u32, 5 i32, 6 f32, 7 bool, 8 string, 9 array,
+ * 10 u64, 11 i64, 12 f64 (arrays: element type and count) */
+int qg_gguf_kv_info(const qg_gguf* file, int64_t index, const char** key, int* type, uint64_t* array_count,
+                    int* array_type);
+int qg_gguf_kv_int(const qg_gguf* file, int64_t index, int64_t* value);
+int qg_gguf_kv_float(const qg_gguf* file, int64_t index, double* value);
+int qg_gguf_kv_string(const qg_gguf* file, int64_t index, const char** str, uint64_t* len);  /* not NUL-terminated */
 
 /* ---- introspection ---- */
 const char* qg_status_string(int status);

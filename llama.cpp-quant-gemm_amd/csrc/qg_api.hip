@@ -107,6 +107,32 @@ int run_w16(int wtype, const float* A, const void* B, float* C, int M, int N, in
     return hip_status(launch_w16(g, st));
 }
 
+// Dims as extract_dims_from_tensor (include/llama_adapter.h:49-61): K = act->ne[0], M = act->ne[1],
+// N = w->ne[1]; output [N, M] in ggml ne-order, i.e. row-major C[M][N]. Rows must be dense (the
+// kernels' layout); batched views (ne[2..3] > 1) are out of scope. k_mult: K granularity.
+size_t row_bytes(int type, int64_t K) {
+    if (type == QG_TYPE_F32) return (size_t)K * 4;
+    if (type == QG_TYPE_F16) return (size_t)K * 2;
+    return (size_t)(K / 32) * (size_t)block_bytes(type);
+}
+
+int view_dims(const qg_tensor_view* act, const qg_tensor_view* w, const qg_tensor_view* out, int64_t& M, int64_t& N,
+              int64_t& K, int k_mult = 32) {
+    for (int d = 2; d < 4; ++d)
+        if ((act->ne[d] != 1 && act->ne[d] != 0) || (w->ne[d] != 1 && w->ne[d] != 0) || (out->ne[d] != 1 && out->ne[d] != 0))
+            return QG_ERR_UNSUPPORTED;
+    K = act->ne[0];
+    M = act->ne[1];
+    N = w->ne[1];
+    if (w->ne[0] != K || out->ne[0] != N || out->ne[1] != M) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % k_mult != 0) return QG_ERR_BAD_K;
+    if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return QG_ERR_UNSUPPORTED;
+    if ((M > 1 && act->nb[1] != row_bytes(act->type, K)) || (N > 1 && w->nb[1] != row_bytes(w->type, K)) ||
+        out->nb[0] != sizeof(float) || (M > 1 && out->nb[1] != (size_t)N * sizeof(float)))
+        return QG_ERR_UNSUPPORTED;
+    return QG_OK;
+}
+
 size_t fused_workspace_bytes(int M, int K) { return M > 0 && K > 0 ? (size_t)M * (size_t)(K / 32) * 36 : 0; }
 
 // FP32 / FP16 activations (g.ain != AIN_Q8_1), dense rows of K elements. Small M: quantization
@@ -294,20 +320,57 @@ int qg_gemm_w4a8_from_view(const qg_tensor_view* act, const qg_tensor_view* w, q
         else if (strcmp(kernel_type, "generic") == 0) algo = QG_ALGO_GENERIC;
         else return QG_ERR_INVALID_ARG;
     }
-    // Dims as extract_dims_from_tensor (include/llama_adapter.h:49-61): M = act->ne[1],
-    // K = act->ne[0], N = w->ne[1].
     if (act->type != QG_TYPE_Q8_1 || out->type != QG_TYPE_F32 || !is_weight_type(w->type)) return QG_ERR_UNSUPPORTED;
-    for (int d = 2; d < 4; ++d)
-        if ((act->ne[d] != 1 && act->ne[d] != 0) || (w->ne[d] != 1 && w->ne[d] != 0) || (out->ne[d] != 1 && out->ne[d] != 0))
-            return QG_ERR_UNSUPPORTED;  // batched (ne[2..3] > 1) views are out of scope
-    const int64_t K = act->ne[0], M = act->ne[1], N = w->ne[1];
-    if (w->ne[0] != K || out->ne[0] != N || out->ne[1] != M) return QG_ERR_INVALID_ARG;
-    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
-    // Rows must be dense (blocks contiguous within and across rows), as the kernels assume.
-    if (act->nb[1] != (size_t)(K / 32) * 36 || w->nb[1] != (size_t)(K / 32) * block_bytes(w->type) ||
-        out->nb[0] != sizeof(float) || (M > 1 && out->nb[1] != (size_t)N * sizeof(float)))
-        return QG_ERR_UNSUPPORTED;
+    int64_t M, N, K;
+    const int rc = view_dims(act, w, out, M, N, K);
+    if (rc != QG_OK) return rc;
     return qg_gemm_w4a8_ex(act->data, w->data, (float*)out->data, (int)M, (int)N, (int)K, w->type, algo, stream);
+}
+
+int qg_gemm_w4a16_from_view(const qg_tensor_view* act, const qg_tensor_view* w, qg_tensor_view* out,
+                            const char* kernel_type, qg_stream_t stream) {
+    if (!act || !w || !out) return QG_ERR_INVALID_ARG;
+    if (kernel_type && strcmp(kernel_type, "naive") != 0 && strcmp(kernel_type, "tiled") != 0 &&
+        strcmp(kernel_type, "auto") != 0)
+        return QG_ERR_INVALID_ARG;
+    if (act->type != QG_TYPE_F32 || out->type != QG_TYPE_F32 || (w->type != QG_TYPE_Q4_0 && w->type != QG_TYPE_Q8_0))
+        return QG_ERR_UNSUPPORTED;
+    int64_t M, N, K;
+    const int rc = view_dims(act, w, out, M, N, K);
+    if (rc != QG_OK) return rc;
+    return run_w16(w->type, (const float*)act->data, w->data, (float*)out->data, (int)M, (int)N, (int)K,
+                   (hipStream_t)stream);
+}
+
+int qg_gemm_fp32_from_view(const qg_tensor_view* act, const qg_tensor_view* w, qg_tensor_view* out,
+                           const char* kernel_type, qg_stream_t stream) {
+    if (!act || !w || !out) return QG_ERR_INVALID_ARG;
+    if (kernel_type && strcmp(kernel_type, "naive") != 0 && strcmp(kernel_type, "tiled") != 0 &&
+        strcmp(kernel_type, "auto") != 0)
+        return QG_ERR_INVALID_ARG;
+    if (act->type != QG_TYPE_F32 || out->type != QG_TYPE_F32 || w->type != QG_TYPE_F32) return QG_ERR_UNSUPPORTED;
+    int64_t M, N, K;
+    const int rc = view_dims(act, w, out, M, N, K, 1);
+    if (rc != QG_OK) return rc;
+    return qg_gemm_fp32((const float*)act->data, (const float*)w->data, (float*)out->data, (int)M, (int)N, (int)K,
+                        stream);
+}
+
+int qg_validate_view_types(const qg_tensor_view* act, const qg_tensor_view* w, const qg_tensor_view* out,
+                           int expected_activation_type, int expected_weight_type, int expected_output_type) {
+    return act && w && out && act->type == expected_activation_type && w->type == expected_weight_type &&
+           out->type == expected_output_type;
+}
+
+int qg_gemm_fp32(const float* A, const float* B, float* C, int M, int N, int K, qg_stream_t stream) {
+    if (M < 0 || N < 0 || K < 0) return QG_ERR_INVALID_ARG;
+    if (M == 0 || N == 0) return QG_OK;
+    if (!A || !B || !C) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)A & 3) != 0 || ((uintptr_t)B & 3) != 0 || ((uintptr_t)C & 3) != 0) return QG_ERR_ALIGN;
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K;
+    g.ldc_m = N; g.ldc_n = 1;
+    return hip_status(launch_fp32(g, (hipStream_t)stream));
 }
 
 const char* qg_status_string(int s) {

@@ -37,6 +37,9 @@ hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.
 hipError_t launch_w16(const GemmArgs& g, hipStream_t st);
 
+// FP32 GEMM C = A . B^T (the unquantized baseline), A = float[M][K], B = float[N][K].
+hipError_t launch_fp32(const GemmArgs& g, hipStream_t st);
+
 // Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);
 // FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143).

@@ -47,6 +47,28 @@ SIGNATURES = {
     "qg_dequantize_q4_0": ([P, P, I64, P], I),
     "qg_debug_sumi": ([P, P, P, I, I, I, I, I, P], I),
     "qg_gemm_w4a8_from_view": ([P, P, P, ctypes.c_char_p, P], I),
+    "qg_gemm_w4a16_from_view": ([P, P, P, ctypes.c_char_p, P], I),
+    "qg_gemm_fp32_from_view": ([P, P, P, ctypes.c_char_p, P], I),
+    "qg_validate_view_types": ([P, P, P, I, I, I], I),
+    "qg_gemm_fp32": ([P, P, P, I, I, I, P], I),
+    "qg_gguf_open": ([ctypes.c_char_p, ctypes.POINTER(P)], I),
+    "qg_gguf_close": ([P], None),
+    "qg_gguf_version": ([P], I),
+    "qg_gguf_alignment": ([P], I64),
+    "qg_gguf_tensor_count": ([P], I64),
+    "qg_gguf_find_tensor": ([P, ctypes.c_char_p], I64),
+    "qg_gguf_tensor_info": ([P, I64, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(I), ctypes.POINTER(I),
+                             ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_uint64)], I),
+    "qg_gguf_tensor_data": ([P, I64], P),
+    "qg_gguf_upload_tensor": ([P, I64, P, SZ, P], I),
+    "qg_gguf_tensor_view": ([P, I64, P, P], I),
+    "qg_gguf_kv_count": ([P], I64),
+    "qg_gguf_find_kv": ([P, ctypes.c_char_p], I64),
+    "qg_gguf_kv_info": ([P, I64, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(I), ctypes.POINTER(ctypes.c_uint64),
+                         ctypes.POINTER(I)], I),
+    "qg_gguf_kv_int": ([P, I64, ctypes.POINTER(I64)], I),
+    "qg_gguf_kv_float": ([P, I64, ctypes.POINTER(ctypes.c_double)], I),
+    "qg_gguf_kv_string": ([P, I64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)], I),
     "qg_status_string": ([I], ctypes.c_char_p),
     "qg_last_hip_error": ([], I),
     "qg_select_algo": ([I, I, I, I], I),
