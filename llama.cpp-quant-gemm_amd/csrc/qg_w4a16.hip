@@ -14,7 +14,8 @@
 // of one weight row (register-resident decode), the activations are staged once per workgroup
 // into LDS records [m][unit][BPL x 32 floats] (+4 dwords pad: the 16 lanes of a ds_read_b128 group
 // read units at a stride of 4 x odd dwords, distinct bank slots), rows reduce with DPP. M > 8
-// runs as chunks of 8 activation rows on blockIdx.y (the weights are streamed once per chunk).
+// runs on the matrix cores instead (w16_mfma_kernel below; the GEMV's row chunks remain for
+// activations that are not 16-B aligned).
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
 
@@ -171,9 +172,171 @@ __global__ __launch_bounds__(256) void w16_generic_kernel(const float* __restric
     if (lane == 63) C[m * ldc_m + n * ldc_n] = acc;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Prefill (M > 8): bf16 MFMA with exact operands. A Q4_0 / Q8_0 weight code minus its offset
+// (q - 8, or the signed Q8_0 byte) is an exact bf16; an fp32 activation is split exactly into three
+// bf16 parts, a = hi + mid + lo (each the truncated top 8 significant bits of what is left; 24 bits
+// in all). Per block and 16 x 16 tile, three chained v_mfma_f32_16x16x32_bf16 (K = 32 = one block)
+// accumulate sum_k w_k (hi_k + mid_k + lo_k) in fp32 — the block's exact-product dot — and the
+// epilogue adds d_w * dot into the output accumulator. Operand maps (cdna_hip_programming.md §3):
+// lane l holds A[row l&15][k = 8(l>>4) + j] and B[k][col l&15]; C col = l&15, row = 4(l>>4) + e.
+// Here k = element index within the block, rows = weight rows, cols = tokens.
+// A workgroup owns 16 RT rows x 16 TT tokens; its W waves split the blocks round-robin (the next
+// block's loads in flight while the current one computes); partial tiles are summed in fixed wave
+// order through LDS at the end.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t hi16_pack(uint32_t lo_elem, uint32_t hi_elem) {
+    return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // {lo_elem[31:16], hi_elem[31:16]}
+}
+
+// 8 fp32 activations -> hi / mid / lo bf16 fragments with a = hi + mid + lo exactly
+__device__ __forceinline__ void w16_afrag(const float4 x0, const float4 x1, u32x4_t& h, u32x4_t& m, u32x4_t& l) {
+    const float a[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    uint32_t hb[8], mb[8], lb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hb[j] = __float_as_uint(a[j]) & 0xFFFF0000u;
+        const float r1 = a[j] - __uint_as_float(hb[j]);
+        mb[j] = __float_as_uint(r1) & 0xFFFF0000u;
+        const float r2 = r1 - __uint_as_float(mb[j]);
+        lb[j] = __float_as_uint(r2);  // <= 8 significant bits left: its top half is exact
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        h[p] = hi16_pack(hb[2 * p], hb[2 * p + 1]);
+        m[p] = hi16_pack(mb[2 * p], mb[2 * p + 1]);
+        l[p] = hi16_pack(lb[2 * p], lb[2 * p + 1]);
+    }
+}
+
+template <int F, int RT, int TT, int W>
+__global__ __launch_bounds__(W * 64) void w16_mfma_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
+                                                          float* __restrict__ C, int M, int N, int K, long ldc_m,
+                                                          long ldc_n) {
+    using T = wfmt<F>;
+    constexpr int NACC = RT * TT * 4;
+    extern __shared__ __attribute__((aligned(16))) float red[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int n0 = blockIdx.x * 16 * RT, m0 = blockIdx.y * 16 * TT;
+    const int nb = K / QK;
+    const long RB = (long)nb * T::BB;
+
+    const uint8_t* wrow[RT];
+    const float* arow[TT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) wrow[i] = B + (long)min(n0 + 16 * i + r16, N - 1) * RB;
+#pragma unroll
+    for (int t = 0; t < TT; ++t) arow[t] = A + (long)min(m0 + 16 * t + r16, M - 1) * K + 8 * q;
+
+    struct raw_t {
+        uint32_t wq[RT][2];
+        uint32_t wd[RT];
+        float4 a[TT][2];
+    };
+    auto load = [&](raw_t& r, int b) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const uint8_t* blk = wrow[i] + (long)b * T::BB;
+            __builtin_memcpy(r.wq[i], blk + 2 + (T::Q8 ? 8 * q : 8 * (q & 1)), 8);
+            r.wd[i] = *reinterpret_cast<const uint16_t*>(blk);
+        }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const float4* p = reinterpret_cast<const float4*>(arow[t] + b * QK);
+            r.a[t][0] = p[0];
+            r.a[t][1] = p[1];
+        }
+    };
+
+    float acc[NACC];
+#pragma unroll
+    for (int x = 0; x < NACC; ++x) acc[x] = 0.0f;
+
+    raw_t cur, nxt;
+    if (wave < nb) load(cur, wave);
+    for (int b = wave; b < nb; b += W) {
+        if (b + W < nb) load(nxt, b + W);
+        u32x4_t wf[RT], ah[TT], am[TT], al[TT];
+        float dw[RT][4];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            float v[8];
+            if constexpr (T::Q8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (float)(int)(int8_t)(cur.wq[i][j / 4] >> (8 * (j & 3)));
+            } else {
+                const int sh = (q >> 1) * 4;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (float)((cur.wq[i][j / 4] >> (8 * (j & 3) + sh)) & 0xFu) - 8.0f;
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) wf[i][p] = hi16_pack(__float_as_uint(v[2 * p]), __float_as_uint(v[2 * p + 1]));
+            const float d_own = h2f(cur.wd[i]);  // this lane's row r16
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dw[i][e] = __shfl(d_own, 4 * q + e);  // rows 4q + e
+        }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) w16_afrag(cur.a[t][0], cur.a[t][1], ah[t], am[t], al[t]);
+        f32x4_t c[RT][TT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                c[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[i]),
+                                                                  __builtin_bit_cast(bf16x8_t, ah[t]),
+                                                                  f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                c[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[i]),
+                                                                  __builtin_bit_cast(bf16x8_t, am[t]), c[i][t], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                c[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[i]),
+                                                                  __builtin_bit_cast(bf16x8_t, al[t]), c[i][t], 0, 0, 0);
+        // MFMA results read by the VALU only behind an explicit wait (see qg_mmq_kernel.hpp)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float ce = c[i][t][e];
+                    acc[(i * TT + t) * 4 + e] = __builtin_fmaf(dw[i][e], ce, acc[(i * TT + t) * 4 + e]);
+                }
+        if (b + W < nb) cur = nxt;
+    }
+
+    // fixed-order sum of the W partial tiles
+#pragma unroll
+    for (int x = 0; x < NACC; ++x) red[(wave * NACC + x) * 64 + lane] = acc[x];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < NACC * 64; idx += W * 64) {
+        float v = red[idx];
+#pragma unroll
+        for (int ww = 1; ww < W; ++ww) v += red[ww * NACC * 64 + idx];
+        const int x = idx >> 6, ln = idx & 63;
+        const int e = x & 3, t = (x >> 2) % TT, i = (x >> 2) / TT;
+        const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
+        const int m = m0 + 16 * t + (ln & 15);
+        if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
+    }
+}
+
 namespace {
 constexpr int W16_MT = 8;
-constexpr size_t W16_LDS_MAX = 128 * 1024;
+constexpr size_t W16_LDS_MAX = 160 * 1024;
 
 template <int F, int BPL> size_t w16_lds(int mt, int K) { return (size_t)mt * (K / QK / BPL) * w16_geom<F, BPL>::REC_DW * 4; }
 
@@ -202,23 +365,39 @@ template <int F, int MT> hipError_t w16_launch_mt(const GemmArgs& g, hipStream_t
     return w16_launch<F, MT, 2, 8, 256>(g, st);
 }
 
-template <int F> bool w16_fast_ok(const GemmArgs& g) {
+// Rows per chunk: the next power of two >= M (at most 8), halved until the LDS records fit; 0 if
+// the fast kernel does not apply (alignment, K not a multiple of 64).
+template <int F> int w16_pick_mt(const GemmArgs& g) {
     const int nb = g.K / QK;
     const int bpl = nb % 4 == 0 ? 4 : 2;
-    if (nb % bpl != 0) return false;
-    if (((uintptr_t)g.A & 15) != 0 || ((uintptr_t)g.B & 3) != 0) return false;
-    if ((g.M + W16_MT - 1) / W16_MT > 65535) return false;
-    const int mt = g.M < W16_MT ? (g.M <= 1 ? 1 : g.M <= 2 ? 2 : g.M <= 4 ? 4 : W16_MT) : W16_MT;
-    const size_t lds = bpl == 4 ? w16_lds<F, 4>(mt, g.K) : w16_lds<F, 2>(mt, g.K);
-    return lds <= W16_LDS_MAX;
+    if (nb % bpl != 0) return 0;
+    if (((uintptr_t)g.A & 15) != 0 || ((uintptr_t)g.B & 3) != 0) return 0;
+    for (int mt = g.M <= 1 ? 1 : g.M <= 2 ? 2 : g.M <= 4 ? 4 : W16_MT; mt >= 1; mt /= 2) {
+        const size_t lds = bpl == 4 ? w16_lds<F, 4>(mt, g.K) : w16_lds<F, 2>(mt, g.K);
+        if (lds <= W16_LDS_MAX && (g.M + mt - 1) / mt <= 65535) return mt;
+    }
+    return 0;
+}
+
+template <int F, int RT, int TT, int W> hipError_t w16_mfma_launch(const GemmArgs& g, hipStream_t st) {
+    const dim3 grid((g.N + 16 * RT - 1) / (16 * RT), (g.M + 16 * TT - 1) / (16 * TT));
+    const size_t lds = (size_t)W * RT * TT * 4 * 64 * 4;
+    hipLaunchKernelGGL((w16_mfma_kernel<F, RT, TT, W>), grid, dim3(W * 64), lds, st, (const float*)g.A,
+                       (const uint8_t*)g.B, g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n);
+    return hipGetLastError();
 }
 
 template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
-    if (w16_fast_ok<F>(g)) {
-        if (g.M <= 1) return w16_launch_mt<F, 1>(g, st);
-        if (g.M <= 2) return w16_launch_mt<F, 2>(g, st);
-        if (g.M <= 4) return w16_launch_mt<F, 4>(g, st);
-        return w16_launch_mt<F, W16_MT>(g, st);
+    if (g.M > 8 && ((uintptr_t)g.A & 15) == 0 && (g.M + 31) / 32 <= 65535) {
+        // one 16-row tile per workgroup while that leaves < 256 workgroups of 32 rows
+        if ((long)((g.N + 31) / 32) * ((g.M + 31) / 32) < 256) return w16_mfma_launch<F, 1, 2, 16>(g, st);
+        return w16_mfma_launch<F, 2, 2, 16>(g, st);
+    }
+    switch (w16_pick_mt<F>(g)) {
+        case 1: return w16_launch_mt<F, 1>(g, st);
+        case 2: return w16_launch_mt<F, 2>(g, st);
+        case 4: return w16_launch_mt<F, 4>(g, st);
+        case 8: return w16_launch_mt<F, 8>(g, st);
     }
     if (g.M > 65535) return hipErrorInvalidValue;
     hipLaunchKernelGGL(w16_generic_kernel<F>, dim3((g.N + 3) / 4, g.M), dim3(256), 0, st, (const float*)g.A,

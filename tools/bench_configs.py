@@ -26,9 +26,14 @@ PEAK = 8000.0
 CONFIGS = [
     ("q4_0", 1, 4096, 4096), ("q4_1", 1, 4096, 4096), ("q5_0", 1, 4096, 4096), ("q5_1", 1, 4096, 4096),
     ("q4_0", 32, 4096, 4096), ("q4_0", 1, 32000, 4096), ("q4_0", 1, 4000, 4096),
-    ("q4_0", 8, 4096, 4096), ("q4_0", 1, 4096, 14336), ("q4_0", 2, 4096, 14336), ("q4_0", 512, 4096, 4096),
+    ("q4_0", 8, 4096, 4096), ("q4_0", 1, 4096, 14336), ("q4_0", 2, 4096, 14336), ("q4_0", 64, 4096, 4096),
+    ("q4_0", 128, 4096, 4096), ("q4_0", 512, 4096, 4096),
+    ("q8_0", 1, 4096, 4096), ("q8_0", 32, 4096, 4096),          # W8A8
+    ("w4a16", 1, 4096, 4096), ("w4a16", 4, 4096, 4096), ("w4a16", 32, 4096, 4096), ("w4a16", 512, 4096, 4096),
+    ("w8a16", 1, 4096, 4096), ("w8a16", 32, 4096, 4096),
 ]
-WT = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
+WT = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7, "q8_0": 8}
+W16 = {"w4a16": 2, "w8a16": 8}
 
 
 def graph_us(step, reps: int) -> float:
@@ -51,7 +56,45 @@ def graph_us(step, reps: int) -> float:
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
+def measure_w16(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
+    """FP32 activations x Q4_0 / Q8_0 weights (qg_gemm_w4a16 / qg_gemm_w8a16)."""
+    dev = torch.device("cuda", 0)
+    wt = W16[wname]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    a = torch.rand((M, K), generator=gen, device=dev) * 2 - 1
+    b = torch.rand((N, K), generator=gen, device=dev) * 2 - 1
+    bq = qg.quantize(b, wt)
+    fn = qg.gemm_w4a16 if wt == 2 else qg.gemm_w8a16
+    c = fn(a, bq, M, N, K)
+    ref = a.double() @ b.double().T
+    nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
+    del b, ref
+    wbytes = bq.numel()
+    R = max(2, math.ceil(600e6 / wbytes))
+    G = min(G, R)
+    copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
+    copies.copy_(bq.unsqueeze(0).expand_as(copies))
+    out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+    lib = qg._lib.load()
+    sym = lib.qg_gemm_w4a16 if wt == 2 else lib.qg_gemm_w8a16
+
+    def step(stream):
+        for j in range(G):
+            assert sym(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                       ctypes.c_void_p(out[j].data_ptr()), M, N, K, stream) == 0
+
+    us = graph_us(step, reps) / G
+    byts = wbytes + M * K * 4 + M * N * 4
+    flops = 2.0 * M * N * K
+    return {"wtype": wname, "M": M, "N": N, "K": K, "algo": "w16 gemv", "us_per_launch": round(us, 3),
+            "gbps": round(byts / us / 1e3, 1), "frac_hbm": round(byts / us / 1e3 / PEAK, 4),
+            "tflops": round(flops / us / 1e6, 3), "nmse_vs_fp32": nmse, "algorithmic_bytes": byts, "launches": G}
+
+
 def measure(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
+    if wname in W16:
+        return measure_w16(wname, M, N, K, G, reps)
     dev = torch.device("cuda", 0)
     wt = WT[wname]
     bb = qg.BLOCK_BYTES[wt]
@@ -137,9 +180,13 @@ def main() -> None:
     ap.add_argument("--out", default=None)
     ap.add_argument("--gemvs", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default=None, help="comma-separated weight kinds to run (e.g. w4a16,q8_0)")
     args = ap.parse_args()
     rows = []
+    only = set(args.only.split(",")) if args.only else None
     for w, m, n, k in CONFIGS:
+        if only and w not in only:
+            continue
         r = measure(w, m, n, k, args.gemvs, args.reps)
         print(json.dumps(r), flush=True)
         rows.append(r)
