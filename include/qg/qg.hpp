@@ -61,6 +61,46 @@ inline int gemm_q5_1_q8_1(const qg_block_q5_1* W, const qg_block_q8_1* A, float*
     return qg_gemm_q5_1_q8_1(W, A, out, M, N, K, stream);
 }
 
+inline int gemm_q8_0_q8_1(const qg_block_q8_0* W, const qg_block_q8_1* A, float* out, int M, int N, int K,
+                          qg_stream_t stream = nullptr) {  // gemm_quant_formats.cuh:415
+    return qg_gemm_q8_0_q8_1(W, A, out, M, N, K, stream);
+}
+
+// W8A8, activation-major (gemm_cuda_naive.cuh:294, gemm_cuda_dp4a.cuh:418)
+inline int gemm_w8a8_naive(const qg_block_q8_1* A, const qg_block_q8_0* B, float* C, int M, int N, int K,
+                           qg_stream_t stream = nullptr) {
+    return qg_gemm_w8a8(A, B, C, M, N, K, stream);
+}
+inline int gemm_w8a8_dp4a(const qg_block_q8_1* A, const qg_block_q8_0* B, float* C, int M, int N, int K,
+                          qg_stream_t stream = nullptr) {
+    return qg_gemm_w8a8(A, B, C, M, N, K, stream);
+}
+
+// FP32 activations (gemm_cuda_naive.cuh:258-283, gemm_cuda_tiled.cuh:284)
+inline int gemm_fp32_naive(const float* A, const float* B, float* C, int M, int N, int K,
+                           qg_stream_t stream = nullptr) {
+    return qg_gemm_fp32(A, B, C, M, N, K, stream);
+}
+inline int gemm_w4a16_naive(const float* A, const qg_block_q4_0* B, float* C, int M, int N, int K,
+                            qg_stream_t stream = nullptr) {
+    return qg_gemm_w4a16(A, B, C, M, N, K, stream);
+}
+inline int gemm_w4a16_tiled(const float* A, const qg_block_q4_0* B, float* C, int M, int N, int K,
+                            qg_stream_t stream = nullptr) {
+    return qg_gemm_w4a16(A, B, C, M, N, K, stream);
+}
+inline int gemm_w8a16_naive(const float* A, const qg_block_q8_0* B, float* C, int M, int N, int K,
+                            qg_stream_t stream = nullptr) {
+    return qg_gemm_w8a16(A, B, C, M, N, K, stream);
+}
+
+// kernels/gemm/gemm_fused.cuh:311-338 — FP16 activations quantized inside the product
+// (half = IEEE binary16 bits; the reference's `half` type)
+inline int gemm_q4_0_fp16_fused(const qg_block_q4_0* weight, const uint16_t* fp16_activation, float* output, int M,
+                                int N, int K, qg_stream_t stream = nullptr) {
+    return qg_gemm_q4_0_fp16_fused(weight, fp16_activation, output, M, N, K, stream);
+}
+
 // include/quantize.h:343-368 — k = number of elements
 inline int quantize_q4_0_cuda(const float* x, qg_block_q4_0* y, int64_t k, qg_stream_t stream = nullptr) {
     return qg_quantize_q4_0(x, y, k, stream);
