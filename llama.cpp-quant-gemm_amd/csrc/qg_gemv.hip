@@ -13,10 +13,10 @@ template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK;
     if (nb % 4 == 0) {
-        if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, 4 * MT, SUMI, AIN>(g, st);
-        return gemv_launch<F, MT, 4, 4, 256, 8 * MT, SUMI, AIN>(g, st);
+        if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);
+        return gemv_launch<F, MT, 4, 4, 256, SUMI, AIN>(g, st);
     }
-    return gemv_launch<F, MT, 2, 8, 256, 8 * MT, SUMI, AIN>(g, st);
+    return gemv_launch<F, MT, 2, 8, 256, SUMI, AIN>(g, st);
 }
 
 template <int F, int AIN> hipError_t launch_m(const GemmArgs& g, hipStream_t st) {

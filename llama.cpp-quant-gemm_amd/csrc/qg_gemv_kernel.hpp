@@ -7,24 +7,37 @@
 //
 // Work decomposition:
 //  * A lane owns "units" of BPL consecutive Q-blocks of one weight row (BPL*BB bytes, e.g. Q4_0
-//    BPL=4 -> 72 B; the compiler issues them as 4 x dwordx4 + 1 x dwordx2). LPR lanes share a row
-//    and stride over its units (the next unit in flight while the current one computes); 64/LPR
-//    rows per wave, WGS/64 waves per workgroup.
-//  * The workgroup stages the M Q8_1 rows once into LDS records (8 qs dwords, f32 d, f32 s, pad;
-//    dword stride 12*BPL+4 per (m, unit) = 4 x odd, so the 16 lanes of a ds_read_b128 group hit
-//    distinct bank slots). The activation loads are issued before the weight stream, so the
-//    staging waits only on them.
-//  * Blocks are decoded in registers with compile-time alignbyte/shift/mask (qg_common.hpp) and
-//    dotted with v_dot4c_i32_i8: exact int32 sumi; the per-block epilogue is the reference's
-//    operation order, no contraction -> block terms bit-identical to the CPU oracle.
+//    BPL=4 -> 72 B; 4 x dwordx4 + 1 x dwordx2). LPR lanes share a row and stride over its units
+//    (the next unit in flight while the current one computes); 64/LPR rows per wave, WGS/64 waves
+//    per workgroup.
+//  * The workgroup stages the M activation rows once into LDS, one 12-dword record per Q8_1 block
+//    (one thread per block; unit stride 12*BPL+4 dwords = 4 x odd, so the 16 lanes of a
+//    ds_read_b128 group hit distinct bank slots). The first block's loads are issued before the
+//    weight stream, so the staging waits only on them.
+//  * Integer dot, exact int32 sumi, two forms:
+//      - nibble planes (Q4_0, Q4_1 weights): each activation byte a = 16*h + l with h = a >> 4
+//        (signed 4-bit) and l = a & 15; the record holds the l and h nibbles of elements
+//        (4i+k, 16+4i+k) interleaved exactly like the weight nibbles of qs dword i, so one raw
+//        weight dword q feeds v_dot8_u32_u4(q, l) and, XORed with 0x88888888 (= signed q - 8),
+//        v_dot8_i32_i4(q^0x8.., h): sumi = L + 16*H + 128*sum(h), the last term (activation only)
+//        folded into the accumulator's initial value. 8 dot8 + 4 XOR per block, no nibble
+//        unpacking;
+//      - bytes (Q5_0, Q5_1, Q8_0): blocks decoded in registers with compile-time
+//        alignbyte/shift/mask (qg_common.hpp), 8 v_dot4c_i32_i8 per block.
+//    Both accumulate on top of the bit pattern of 1.5*2^23, so the int32 result read as f32 is
+//    1.5*2^23 + sumi (|sumi| < 2^22): no int->float convert.
+//  * Per-block epilogue in the reference's operation order, so each block's fp32 term is
+//    bit-identical to the CPU oracle's: fma(d_a, cf, -1.5*2^23*d_a) = round(d_a*sumi) (the
+//    constant is exact), c*s_a precomputed in the record (exact: c is 8, 16 or 1), d_w (and m_w)
+//    taken straight from the f16 bits by v_fma_mix_f32 with a zero addend (= one rounding of the
+//    f32 product, as the reference's d_w * (...)).
 //  * Per-lane partials (unit order, block order) are reduced across the row's LPR lanes with DPP
-//    row ops (group_sum_last: no LDS round trips — the ds_bpermute chain it replaced was ~0.1 us of
-//    a 4 us launch); the row's last lane stores. Deterministic.
+//    row ops (group_sum_last); the row's last lane stores. Deterministic.
 //  * AIN != 0 (fused activation quantization): A is FP32 (AIN_F32, quantized as
 //    quantize_row_q8_1_ref) or FP16 (AIN_F16_FUSED, as kernels/gemm/gemm_fused.cuh:76-143) [M][K];
-//    each thread quantizes whole 32-element blocks straight into the LDS records
-//    (qg_quant_block.hpp), so the records — and every output — are bit-identical to the two-step
-//    quantize + GEMV path. The first block's loads are issued before the weight stream.
+//    each thread quantizes whole 32-element blocks (qg_quant_block.hpp) and builds the same LDS
+//    record, so every output is bit-identical to the two-step quantize + GEMV path.
+//  * NT: the weight stream is loaded with the nontemporal hint (read once per launch).
 // Tuning record (probes, per-wave timelines, rejected designs): profiles/r01_tuning/README.md.
 #pragma once
 #include "qg_common.hpp"
@@ -33,12 +46,109 @@
 
 namespace qg {
 
+constexpr uint32_t ACC_BIAS = 0x4B400000u;  // bits of 12582912.0f = 1.5 * 2^23
+constexpr float ACC_BIAS_F = 12582912.0f;
+
 template <int F, int BPL> struct gemv_geom {
     static constexpr int BB = wfmt<F>::BB;
     static constexpr int UB = BPL * BB;          // unit bytes
     static constexpr int UDW = UB / 4;           // unit dwords (BB even, BPL even -> whole dwords)
     static constexpr int REC_DW = 12 * BPL + 4;  // LDS record dwords per (m, unit)
 };
+
+// Nibble-plane dot for Q4_0 / Q4_1 weights (see header).
+template <int F> constexpr bool gemv_planes = F == FMT_Q4_0 || F == FMT_Q4_1;
+// c in the record's c * s_a: Q4_0 -8 s_a, Q5_0 -16 s_a, Q4_1 / Q5_1 + m_w s_a, Q8_0 none.
+template <int F> constexpr float gemv_cs = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : 1.0f;
+
+// x * (f16 value in the low / high half of h), one rounding (v_fma_mix_f32 with a zero addend).
+template <int HI> __device__ __forceinline__ float mixmul(uint32_t h, float x) {
+    float r;
+    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+    else asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+    return r;
+}
+// f16 field at compile-time byte offset OFF of a register-resident byte stream, times x.
+template <int OFF> __device__ __forceinline__ float mixmul_at(const uint32_t* w, float x) {
+    static_assert(OFF % 2 == 0, "fp16 fields are 2-byte aligned");
+    return mixmul<(OFF % 4) / 2>(w[OFF / 4], x);
+}
+
+// The 12-dword LDS record of one Q8_1 block (b[0] = f16 d | f16 s << 16, b[1..8] = qs):
+//   planes: [0..3] l nibbles, [4..7] h nibbles (element pairs (4i+k, 16+4i+k) at nibbles 2k, 2k+1
+//           of dword i), [11] initial accumulator bits 1.5*2^23 + 128*sum(h);
+//   bytes:  [0..7] qs;
+//   both:   [8] d_a, [9] c * s_a, [10] -1.5*2^23 * d_a (fp32).
+template <int F> __device__ __forceinline__ void make_act_record(const uint32_t (&b)[9], uint32_t* rec) {
+    const float d = h2f(b[0] & 0xFFFFu), s = h2f(b[0] >> 16);
+    uint32_t r[12];
+    if constexpr (gemv_planes<F>) {
+        int sh = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t a0 = b[1 + i], a1 = b[5 + i];
+            r[i] = (a0 & 0x0F0F0F0Fu) | ((a1 << 4) & 0xF0F0F0F0u);
+            r[4 + i] = ((a0 >> 4) & 0x0F0F0F0Fu) | (a1 & 0xF0F0F0F0u);
+            sh = __builtin_amdgcn_sdot8((int)r[4 + i], 0x11111111, sh, false);
+        }
+        r[11] = ACC_BIAS + (uint32_t)(128 * sh);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = b[1 + i];
+        r[11] = ACC_BIAS;
+    }
+    r[8] = __float_as_uint(d);
+    r[9] = __float_as_uint(gemv_cs<F> * s);
+    r[10] = __float_as_uint(-(d * ACC_BIAS_F));
+    *reinterpret_cast<uint4*>(rec) = make_uint4(r[0], r[1], r[2], r[3]);
+    *reinterpret_cast<uint4*>(rec + 4) = make_uint4(r[4], r[5], r[6], r[7]);
+    *reinterpret_cast<uint4*>(rec + 8) = make_uint4(r[8], r[9], r[10], r[11]);
+}
+
+// Biased int32 dot (bits of 1.5*2^23 + sumi) of block BI of a register-resident unit with its
+// activation record.
+template <int F, int BI> __device__ __forceinline__ uint32_t block_dot(const uint32_t* w, const uint4 (&a)[3]) {
+    using T = wfmt<F>;
+    constexpr int base = BI * T::BB;
+    if constexpr (gemv_planes<F>) {
+        const uint32_t l[4] = {a[0].x, a[0].y, a[0].z, a[0].w};
+        const uint32_t h[4] = {a[1].x, a[1].y, a[1].z, a[1].w};
+        uint32_t L = a[2].w;
+        int H = 0;
+        static_for<4>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const uint32_t q = ld32<base + T::QS + 4 * i>(w);
+            L = __builtin_amdgcn_udot8(q, l[i], L, false);
+            H = __builtin_amdgcn_sdot8((int)(q ^ 0x88888888u), (int)h[i], H, false);
+        });
+        return L + ((uint32_t)H << 4);
+    } else {
+        const wblock wb = decode_block<F, BI>(w);
+        const uint32_t av[8] = {a[0].x, a[0].y, a[0].z, a[0].w, a[1].x, a[1].y, a[1].z, a[1].w};
+        int s = (int)ACC_BIAS;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = __builtin_amdgcn_sdot4((int)wb.q[i], (int)av[i], s, false);
+        return (uint32_t)s;
+    }
+}
+
+// The reference's per-block term from the biased dot (see header).
+template <int F, int BI> __device__ __forceinline__ float block_term_rec(const uint32_t* w, uint32_t acc, const uint4& sc) {
+    using T = wfmt<F>;
+    constexpr int base = BI * T::BB;
+    const float cf = __uint_as_float(acc);
+    const float da = __uint_as_float(sc.x), cs = __uint_as_float(sc.y), nda = __uint_as_float(sc.z);
+    if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0) {
+        const float t1 = __builtin_fmaf(da, cf, nda);  // d_a * sumi
+        return mixmul_at<base>(w, t1 - cs);             // d_w * (d_a * sumi - c * s_a)
+    } else if constexpr (F == FMT_Q8_0) {
+        return mixmul_at<base>(w, __builtin_fmaf(da, cf, nda));  // (sumi * d_a) * d_w
+    } else {
+        const float fs = cf - ACC_BIAS_F;                             // exact: sumi
+        const float t = mixmul_at<base>(w, da) * fs;                  // (d_w * d_a) * sumi
+        return t + mixmul_at<base + T::MOFF>(w, cs);                  // + m_w * s_a
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // Load the 32 activation values of block g (AIN_F32: 128 B, AIN_F16_FUSED: 64 B; 16-B aligned).
@@ -65,8 +175,10 @@ template <int AIN> __device__ __forceinline__ void load_act_block(const uint8_t*
     }
 }
 
-// NSTAGE: activation dwords per thread loaded before the weight stream (AIN_Q8_1).
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI, int AIN = AIN_Q8_1>
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                    int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
@@ -89,52 +201,43 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
     const uint8_t* wrow = B + (long)(row_ok ? row : 0) * ((long)U * G::UB);
     auto load_unit = [&](uint32_t (&dst)[G::UDW], int u) {
         const uint32_t* p = reinterpret_cast<const uint32_t*>(wrow + (long)((row_ok && u < U) ? u : 0) * G::UB);
+        if constexpr (NT) {
 #pragma unroll
-        for (int v = 0; v < G::UDW; ++v) dst[v] = p[v];
+            for (int v = 0; v + 4 <= G::UDW; v += 4) {
+                const u32x4_a4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4*>(p + v));
+                dst[v] = t.x; dst[v + 1] = t.y; dst[v + 2] = t.z; dst[v + 3] = t.w;
+            }
+            if constexpr (G::UDW % 4 == 2) {
+                const u32x2_a4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2_a4*>(p + G::UDW - 2));
+                dst[G::UDW - 2] = t.x; dst[G::UDW - 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < G::UDW; ++v) dst[v] = p[v];
+        }
     };
-    auto rec_of = [&](int blk) {
-        const int m = blk / nb;
-        const int b = blk - m * nb;
-        const int u = b / BPL;
-        return (m * U + u) * G::REC_DW + (b - u * BPL) * 12;
-    };
+    // record of activation block blk = m * nb + b: unit (m * U + b / BPL) = blk / BPL, slot b % BPL
+    auto rec_of = [&](int blk) { return (blk / BPL) * G::REC_DW + (blk % BPL) * 12; };
     uint32_t cur[G::UDW];
 
+    // 1) activation block loads of this thread (one thread per block), the first before the
+    //    weight stream; 2) the lane's first weight unit; 3) LDS records
+    const int totb = M * nb;
     if constexpr (AIN == AIN_Q8_1) {
-        // 1) activation staging loads first
-        const int tot = M * nb * 9;
-        uint32_t av[NSTAGE];
+        uint32_t ab[9];
+        auto load_ablk = [&](int g) {
+            const uint32_t* p = A + (long)g * 9;
 #pragma unroll
-        for (int i = 0; i < NSTAGE; ++i) {
-            const int g = tid + i * WGS;
-            av[i] = g < tot ? A[g] : 0u;
-        }
-        // 2) weight stream: first unit of this lane
-        load_unit(cur, lir);
-        // 3) activations -> LDS records (the first NSTAGE*WGS dwords were loaded above; a K too
-        //    large for that chunk stages the remainder here, after the weight stream is in flight)
-        auto stage = [&](int g, uint32_t v) {
-            const int blk = g / 9;
-            const int w = g - blk * 9;
-            const int rec = rec_of(blk);
-            if (w == 0) {
-                lds[rec + 8] = __float_as_uint(h2f(v & 0xFFFFu));
-                lds[rec + 9] = __float_as_uint(h2f(v >> 16));
-            } else {
-                lds[rec + w - 1] = v;
-            }
+            for (int i = 0; i < 9; ++i) ab[i] = p[i];
         };
-#pragma unroll
-        for (int i = 0; i < NSTAGE; ++i) {
-            const int g = tid + i * WGS;
-            if (g < tot) stage(g, av[i]);
+        if (tid < totb) load_ablk(tid);
+        load_unit(cur, lir);
+        for (int g = tid; g < totb; g += WGS) {
+            if (g != tid) load_ablk(g);
+            make_act_record<F>(ab, lds + rec_of(g));
         }
-        for (int g = tid + NSTAGE * WGS; g < tot; g += WGS) stage(g, A[g]);
     } else {
-        // Fused quantization: one thread per 32-element block, first block's loads in flight
-        // before the weight stream.
         const uint8_t* X = reinterpret_cast<const uint8_t*>(A);
-        const int totb = M * nb;
         float xv[32];
         if (tid < totb) load_act_block<AIN>(X, tid, xv);
         load_unit(cur, lir);
@@ -143,10 +246,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
             uint32_t w[9];
             if constexpr (AIN == AIN_F32) quantize_q8_1_block<0>(xv, w);
             else quantize_q8_1_block_fp16_fused(xv, w);
-            uint32_t* r = lds + rec_of(g);
-            *reinterpret_cast<uint4*>(r) = make_uint4(w[1], w[2], w[3], w[4]);
-            *reinterpret_cast<uint4*>(r + 4) = make_uint4(w[5], w[6], w[7], w[8]);
-            *reinterpret_cast<float2*>(r + 8) = make_float2(h2f(w[0] & 0xFFFFu), h2f(w[0] >> 16));
+            make_act_record<F>(w, lds + rec_of(g));
         }
     }
     __syncthreads();
@@ -163,20 +263,18 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
         if (u < U) {
             static_for<BPL>([&](auto BI) {
                 constexpr int bi = decltype(BI)::value;
-                const wblock wb = decode_block<F, bi>(cur);
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     if (m < M) {
                         const uint32_t* rec = lds + (m * U + u) * G::REC_DW + bi * 12;
-                        const uint4 a0 = *reinterpret_cast<const uint4*>(rec);
-                        const uint4 a1 = *reinterpret_cast<const uint4*>(rec + 4);
-                        const float2 ds = *reinterpret_cast<const float2*>(rec + 8);
-                        const uint32_t a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                        const int sumi = dot_block(wb.q, a);
+                        const uint4 a[3] = {*reinterpret_cast<const uint4*>(rec),
+                                            *reinterpret_cast<const uint4*>(rec + 4),
+                                            *reinterpret_cast<const uint4*>(rec + 8)};
+                        const uint32_t d = block_dot<F, bi>(cur, a);
                         if constexpr (SUMI) {
-                            if (row_ok) sumi_out[((long)m * N + row) * nb + u * BPL + bi] = sumi;
+                            if (row_ok) sumi_out[((long)m * N + row) * nb + u * BPL + bi] = (int)(d - ACC_BIAS);
                         } else {
-                            acc[m] += block_term<F>(sumi, wb.d, wb.m, ds.x, ds.y);
+                            acc[m] += block_term_rec<F, bi>(cur, d, a[2]);
                         }
                     }
                 }
@@ -204,8 +302,8 @@ template <int F, int BPL> inline size_t gemv_lds_bytes(int M, int K) {
     return (size_t)M * (K / QK / BPL) * gemv_geom<F, BPL>::REC_DW * 4;
 }
 
-// Preconditions of both kernels for unit size BPL: whole units per row, 4-byte aligned operands
-// (units and rows are then whole dwords), LDS records fit (staged kernel).
+// Preconditions of the kernel for unit size BPL: whole units per row, 4-byte aligned operands
+// (units and rows are then whole dwords), LDS records fit.
 template <int F, int BPL>
 inline bool gemv_shape_ok(const GemmArgs& g) {
     if (g.M < 1 || g.M > 8) return false;
@@ -218,12 +316,12 @@ inline bool gemv_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int MT, int BPL, int LPR, int WGS, int NSTAGE, bool SUMI, int AIN = AIN_Q8_1>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false>
 hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
-    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, NSTAGE, SUMI, AIN>;
+    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "gemv_experiments.hpp"  // + the product header qg_gemv_kernel.hpp
+#include "gemv_v1.hpp"           // the round-1 product kernel (A/B baseline)
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -137,7 +138,11 @@ static void bench(Problem& p, std::vector<Variant>& vs, hipStream_t st, int roun
 }
 
 #define STAGED(F, MT, BPL, LPR, WGS, NAME) \
-    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, 4 * MT, false>(g, s); }, false});
+    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false>(g, s); }, false});
+#define STAGED_NT(F, MT, BPL, LPR, WGS, NAME) \
+    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, true>(g, s); }, false});
+#define V1(F, MT, BPL, LPR, WGS, NAME) \
+    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_v1_launch<F, MT, BPL, LPR, WGS, 4 * MT, false>(g, s); }, false});
 #define RAX(F, MT, BPL, LPR, WGS, PF, NAME) \
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_ra_launch<F, MT, BPL, LPR, WGS, PF, false>(g, s); }, false});
 
@@ -152,9 +157,12 @@ static void add_read(std::vector<Variant>& vs, Problem& p) {
 }
 
 template <int F> static void m1(std::vector<Variant>& vs, bool full) {
-    STAGED(F, 1, 4, 32, 512, "staged bpl4 lpr32 wg512")
-    RAX(F, 1, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
-    RAX(F, 1, 4, 32, 256, true, "ra bpl4 lpr32 wg256 pf")
+    V1(F, 1, 4, 32, 512, "v1 bpl4 lpr32 wg512")
+    STAGED(F, 1, 4, 32, 512, "v2 bpl4 lpr32 wg512")
+    STAGED_NT(F, 1, 4, 32, 512, "v2 nt bpl4 lpr32 wg512")
+    STAGED(F, 1, 4, 16, 512, "v2 bpl4 lpr16 wg512")
+    STAGED(F, 1, 4, 32, 256, "v2 bpl4 lpr32 wg256")
+    STAGED_NT(F, 1, 4, 32, 256, "v2 nt bpl4 lpr32 wg256")
     if (full) {
         RAX(F, 1, 4, 32, 128, false, "ra bpl4 lpr32 wg128")
         RAX(F, 1, 4, 32, 512, false, "ra bpl4 lpr32 wg512")
@@ -180,24 +188,28 @@ int main(int argc, char** argv) {
         make(p, s.F, s.M, s.N, s.K, copy);
         std::vector<Variant> vs;
         if (s.M == 1) {
-            const bool full = s.F == FMT_Q4_0;
+            const bool full = false;
             if (s.F == FMT_Q4_0) m1<FMT_Q4_0>(vs, full);
             if (s.F == FMT_Q4_1) m1<FMT_Q4_1>(vs, full);
             if (s.F == FMT_Q5_0) m1<FMT_Q5_0>(vs, full);
             if (s.F == FMT_Q5_1) m1<FMT_Q5_1>(vs, full);
             add_read(vs, p);
         } else if (s.M == 2) {
-            STAGED(FMT_Q4_0, 2, 4, 32, 512, "staged bpl4 lpr32 wg512")
+            V1(FMT_Q4_0, 2, 4, 32, 512, "v1 bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 2, 4, 32, 512, "v2 bpl4 lpr32 wg512")
+            STAGED_NT(FMT_Q4_0, 2, 4, 32, 512, "v2 nt bpl4 lpr32 wg512")
             RAX(FMT_Q4_0, 2, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 2, 4, 32, 256, true, "ra bpl4 lpr32 wg256 pf")
             RAX(FMT_Q4_0, 2, 2, 64, 256, false, "ra bpl2 lpr64 wg256")
         } else if (s.M == 4) {
-            STAGED(FMT_Q4_0, 4, 4, 32, 512, "staged bpl4 lpr32 wg512")
+            V1(FMT_Q4_0, 4, 4, 32, 512, "v1 bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 4, 4, 32, 512, "v2 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 4, 4, 32, 256, "staged bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 2, 64, 256, false, "ra bpl2 lpr64 wg256")
         } else {
-            STAGED(FMT_Q4_0, 8, 4, 32, 512, "staged bpl4 lpr32 wg512")
+            V1(FMT_Q4_0, 8, 4, 32, 512, "v1 bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 8, 4, 32, 512, "v2 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 8, 4, 32, 256, "staged bpl4 lpr32 wg256")
             STAGED(FMT_Q4_0, 8, 2, 64, 512, "staged bpl2 lpr64 wg512")
             RAX(FMT_Q4_0, 8, 2, 64, 256, false, "ra bpl2 lpr64 wg256")

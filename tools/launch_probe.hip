@@ -76,7 +76,7 @@ int main() {
     auto gemv = [&](int copy, hipStream_t s) {
         GemmArgs g;
         g.A = a; g.B = w[copy % R]; g.C = c; g.M = M; g.N = N; g.K = K; g.wtype = FMT_Q4_0; g.ldc_m = N; g.ldc_n = 1;
-        CK((gemv_launch<FMT_Q4_0, 1, 4, 32, 512, 4, false>(g, s)));
+        CK((gemv_launch<FMT_Q4_0, 1, 4, 32, 512, false>(g, s)));
     };
     const int L = 64;
     struct Row { const char* name; std::function<void(int, hipStream_t)> fn; };
