@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "qg_mmq_kernel.hpp"
+#include "mmq_v1.hpp"  // round-1 product kernel (A/B baseline)
 #include "../include/qg/qg.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -63,15 +64,26 @@ int main() {
         // Q4_0 configurations only (other formats: the product dispatch above)
 #define V(BN, TT, W, P16, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, P16>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, st) : hipErrorInvalidValue; }});
-        V(32, 1, 8, true, "mmq bn32 tt1 w8 p16")
-        V(16, 1, 8, true, "mmq bn16 tt1 w8 p16")
-        V(32, 2, 4, true, "mmq bn32 tt2 w4 p16")
-        V(32, 2, 8, true, "mmq bn32 tt2 w8 p16")
-        V(16, 2, 8, true, "mmq bn16 tt2 w8 p16")
-        V(16, 4, 4, true, "mmq bn16 tt4 w4 p16")
-        V(48, 2, 4, true, "mmq bn48 tt2 w4 p16")
-        V(32, 3, 4, true, "mmq bn32 tt3 w4 p16")
-        V(32, 2, 2, true, "mmq bn32 tt2 w2 p16")
+#define V1(BN, TT, W, P16, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_v1_shape_ok<FMT_Q4_0, BN, TT, W, P16>(g) ? mmq_v1_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, st) : hipErrorInvalidValue; }});
+        V1(32, 1, 8, true, "v1 bn32 tt1 w8 p16")
+        V1(16, 1, 8, true, "v1 bn16 tt1 w8 p16")
+        V1(32, 2, 8, true, "v1 bn32 tt2 w8 p16")
+#define VN(BN, TT, W, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB>(g, st) : hipErrorInvalidValue; }});
+        VN(32, 1, 8, 2, "v2 bn32 tt1 w8 nb2")
+        VN(32, 1, 8, 3, "v2 bn32 tt1 w8 nb3")
+        VN(32, 1, 8, 4, "v2 bn32 tt1 w8 nb4")
+        VN(16, 1, 8, 4, "v2 bn16 tt1 w8 nb4")
+        VN(16, 2, 8, 2, "v2 bn16 tt2 w8 nb2")
+        VN(16, 2, 8, 3, "v2 bn16 tt2 w8 nb3")
+        VN(32, 1, 4, 4, "v2 bn32 tt1 w4 nb4")
+        VN(32, 2, 8, 2, "v2 bn32 tt2 w8 nb2")
+        VN(32, 2, 4, 2, "v2 bn32 tt2 w4 nb2")
+        VN(32, 2, 4, 3, "v2 bn32 tt2 w4 nb3")
+        VN(32, 2, 4, 4, "v2 bn32 tt2 w4 nb4")
+        VN(16, 4, 4, 3, "v2 bn16 tt4 w4 nb3")
+#undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
                                  g.wtype = s.F; g.ldc_m = s.N; g.ldc_n = 1; return g; };

@@ -1,4 +1,4 @@
-// qg_mmq_kernel.hpp — W4A8 prefill GEMM (M > 8) on the CDNA4 matrix cores, v_mfma_i32_16x16x32_i8.
+// mmq_v1.hpp — the round-1 product prefill kernel, kept as the A/B baseline of tools/mmq_probe.hip (not the product).
 //
 // C[M,N] = A_q8_1[M,K] . B_w[N,K]^T (include/gemm_reference.h:175-222), activation-major.
 //
@@ -37,30 +37,22 @@
 
 namespace qg {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int v4i_v1 __attribute__((ext_vector_type(4)));
 
-// fma(f16 value in the low half of h, x, c) with one rounding (v_fma_mix_f32).
-__device__ __forceinline__ float fma_mix_lo(uint32_t h, float x, float c) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x), "v"(c));
-    return r;
-}
-
-constexpr int MMQ_BIAS = 0x4B400000;  // bits of 12582912.0f = 1.5 * 2^23
-constexpr float MMQ_BIAS_F = 12582912.0f;
-constexpr int MMQ_SB = 4;             // blocks per stage
+constexpr int MMQ_V1_BIAS = 0x4B400000;  // bits of 12582912.0f = 1.5 * 2^23
+constexpr float MMQ_V1_BIAS_F = 12582912.0f;
+constexpr int MMQ_V1_SB = 4;             // blocks per stage
 
 #ifdef QG_MMQ_STAMPS
 // diagnostic build only (tools/mmq_timeline.hip): per-wave s_memrealtime stamps
-__device__ unsigned long long g_mmq_stamps[8 * 65536];
-#define MMQ_STAMP(k) stamps[k] = __builtin_amdgcn_s_memrealtime()
+__device__ unsigned long long g_mmq_v1_stamps[8 * 65536];
+#define MMQ_V1_STAMP(k) stamps[k] = __builtin_amdgcn_s_memrealtime()
 #else
-#define MMQ_STAMP(k)
+#define MMQ_V1_STAMP(k)
 #endif
 
 // 32 bits at byte offset (compile-time OFF) of an LDS row, from aligned dword reads.
-template <int OFF> __device__ __forceinline__ uint32_t lds32(const uint8_t* base) {
+template <int OFF> __device__ __forceinline__ uint32_t lds32_v1(const uint8_t* base) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (OFF & ~3));
     if constexpr (OFF % 4 == 0) return p[0];
     else return __builtin_amdgcn_alignbyte(p[1], p[0], OFF % 4);
@@ -69,7 +61,7 @@ template <int OFF> __device__ __forceinline__ uint32_t lds32(const uint8_t* base
 // One LDS-DMA instruction: lane's SZ bytes at g -> LDS at (wave-uniform) l + lane * SZ. A __device__
 // function: called straight from a lambda inside the kernel, the builtin made the host pass drop
 // the kernel's launch stub without a diagnostic (undefined symbol at link time).
-template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t* l) {
+template <int SZ> __device__ __forceinline__ void glds_v1(const uint8_t* g, uint8_t* l) {
     auto gp = (const __attribute__((address_space(1))) void*)g;
     auto lp = (__attribute__((address_space(3))) void*)l;
     static_assert(SZ == 4 || SZ == 12 || SZ == 16, "global_load_lds sizes");
@@ -84,53 +76,37 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // window of RIMG bytes and the data sits SHIFT(h) = (h * RSB) % 16 bytes into it. With K % 256 == 0
 // the stage count is even, so the last stage is an odd one (shift 8) and no window reaches past
 // the end of the weight rows.
-// NB: stage buffers per wave (the wave keeps up to NB stages in flight; at M = 32, K = 4096 each
-// wave owns 4 stages, so NB = 4 issues all of its data at once — the kernel was latency-bound with
-// one stage in flight ahead of the one being computed).
-// With 16-B weight pieces the weight and activation pieces of a stage share one piece numbering
-// (p < WPC: weights, then activations), so only the last DMA instruction carries padding.
-template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2> struct mmq_geom {
+template <int F, int BN, int TT, int W, bool P16 = false> struct mmq_v1_geom {
     using T = wfmt<F>;
-    static constexpr int RSB = MMQ_SB * T::BB;                // weight bytes per row per stage
+    static constexpr int RSB = MMQ_V1_SB * T::BB;                // weight bytes per row per stage
     static constexpr int WPS = P16 ? 16 : 4;                   // weight DMA piece (bytes)
     static constexpr int RIMG = P16 && RSB % 16 != 0 ? RSB + 8 : RSB;  // row image bytes
     static constexpr int PPR = RIMG / WPS;                     // pieces per row image
     static constexpr int WPC = BN * PPR;                       // weight pieces per stage
+    static constexpr int NWI = (WPC + 63) / 64;                // weight DMA instructions per stage
     static constexpr int NTOK = 16 * TT;
     static constexpr int APC = NTOK * 9;                       // activation 16-B pieces per stage
-    static constexpr bool CMB = P16;                           // combined piece numbering
-    static constexpr int NWI = CMB ? 0 : (WPC + 63) / 64;      // weight-only DMA instructions
-    static constexpr int NAI = CMB ? 0 : (APC + 63) / 64;      // activation-only DMA instructions
-    static constexpr int NI = CMB ? (WPC + APC + 63) / 64 : NWI + NAI;  // DMA instructions per stage
+    static constexpr int NAI = (APC + 63) / 64;                // activation DMA instructions per stage
+    static constexpr int NI = NWI + NAI;
     static constexpr int RT = BN / 16;                         // row tiles
     // LDS buffer layout (bytes). Every DMA instruction runs on all 64 lanes (see issue()), so the
-    // images are padded to whole instructions.
-    static constexpr int OFF_A = CMB ? WPC * 16 : NWI * 64 * WPS;
-    static constexpr int BUF = CMB ? NI * 64 * 16 : OFF_A + NAI * 64 * 16;
+    // weight and activation images are padded to whole instructions.
+    static constexpr int OFF_A = NWI * 64 * WPS;
+    static constexpr int BUF = OFF_A + NAI * 64 * 16;
     static constexpr int NACC = RT * TT * 4;                   // accumulators per lane
     // wave buffers; the end-of-kernel partial tiles reuse them (after a barrier)
-    static constexpr size_t LDS = (size_t)W * (NB * BUF > NACC * 256 ? NB * BUF : NACC * 256);
-    static_assert(NB >= 2 && NB <= 4, "2..4 stage buffers per wave");
+    static constexpr size_t LDS = (size_t)W * (2 * BUF > NACC * 256 ? 2 * BUF : NACC * 256);
     static_assert(LDS <= 160 * 1024, "LDS per workgroup");
     static_assert(OFF_A % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
     static_assert(RSB % 8 == 0, "stage segments are 8-B multiples");
-    static_assert(NB * NI <= 63, "vmcnt range");
     __host__ __device__ static constexpr int shift(int h) { return P16 ? (h * RSB) & 15 : 0; }
 };
 
-// s_waitcnt vmcnt(younger * NI): the oldest stage's DMA landed, `younger` later stages may still fly.
-template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
-    if (younger <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NI) : "memory");
-}
-
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2>
-__global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+template <int F, int BN, int TT, int W, bool SUMI, bool P16>
+__global__ __launch_bounds__(W * 64) void mmq_v1_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
+    using G = mmq_v1_geom<F, BN, TT, W, P16>;
     using T = wfmt<F>;
     static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -142,40 +118,29 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * G::NTOK;
     const int nb = K / QK;
-    const int H = nb / MMQ_SB;  // stages
+    const int H = nb / MMQ_V1_SB;  // stages
     const long RB = (long)nb * T::BB;
     const long AB = (long)nb * Q8_1_BYTES;
-    uint8_t* bufs = smem + wave * NB * G::BUF;
+    uint8_t* bufs = smem + wave * 2 * G::BUF;
 #ifdef QG_MMQ_STAMPS
     unsigned long long stamps[8] = {};
 #endif
-    MMQ_STAMP(0);
+    MMQ_V1_STAMP(0);
 
     // per-lane DMA source offsets within a stage (rows / tokens past the edge read the last valid
     // one; their results are dropped)
-    auto wpiece = [&](int p) {  // weight piece p of a stage: byte offset in B
+    int woff[G::NWI], aoff[G::NAI];
+#pragma unroll
+    for (int i = 0; i < G::NWI; ++i) {
+        const int p = min(64 * i + lane, G::WPC - 1);
         const int row = p / G::PPR;
-        return (int)((long)min(n0 + row, N - 1) * RB) + (p - row * G::PPR) * G::WPS;
-    };
-    auto apiece = [&](int p) {  // activation piece p of a stage: byte offset in A
+        woff[i] = (int)((long)min(n0 + row, N - 1) * RB) + (p - row * G::PPR) * G::WPS;
+    }
+#pragma unroll
+    for (int i = 0; i < G::NAI; ++i) {
+        const int p = min(64 * i + lane, G::APC - 1);
         const int tok = p / 9;
-        return (int)((long)min(m0 + tok, M - 1) * AB) + (p - tok * 9) * 16;
-    };
-    constexpr int NOFF = G::CMB ? G::NI : 1;
-    int woff[G::CMB ? 1 : G::NWI], aoff[G::CMB ? 1 : G::NAI], coff[NOFF];
-    bool cisw[NOFF];
-    if constexpr (G::CMB) {
-#pragma unroll
-        for (int i = 0; i < G::NI; ++i) {
-            const int p = min(64 * i + lane, G::WPC + G::APC - 1);
-            cisw[i] = p < G::WPC;
-            coff[i] = cisw[i] ? wpiece(p) : apiece(p - G::WPC);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < G::NWI; ++i) woff[i] = wpiece(min(64 * i + lane, G::WPC - 1));
-#pragma unroll
-        for (int i = 0; i < G::NAI; ++i) aoff[i] = apiece(min(64 * i + lane, G::APC - 1));
+        aoff[i] = (int)((long)min(m0 + tok, M - 1) * AB) + (p - tok * 9) * 16;
     }
     // All lanes issue every DMA instruction (lanes past the image fetch a clamped piece into the
     // padding): a lane-predicated global_load_lds let hipcc sink two of them into one block with a
@@ -184,69 +149,53 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = B + (long)h * G::RSB - G::shift(h);
         const uint8_t* asrc = A + (long)h * 144;
-        if constexpr (G::CMB) {
 #pragma unroll
-            for (int i = 0; i < G::NI; ++i) glds<16>((cisw[i] ? wsrc : asrc) + coff[i], buf + 64 * i * 16);
-        } else {
+        for (int i = 0; i < G::NWI; ++i) glds_v1<G::WPS>(wsrc + woff[i], buf + 64 * i * G::WPS);
 #pragma unroll
-            for (int i = 0; i < G::NWI; ++i) glds<G::WPS>(wsrc + woff[i], buf + 64 * i * G::WPS);
-#pragma unroll
-            for (int i = 0; i < G::NAI; ++i) glds<16>(asrc + aoff[i], buf + G::OFF_A + 64 * i * 16);
-        }
+        for (int i = 0; i < G::NAI; ++i) glds_v1<16>(asrc + aoff[i], buf + G::OFF_A + 64 * i * 16);
     };
 
     float acc[G::NACC];
 #pragma unroll
     for (int i = 0; i < G::NACC; ++i) acc[i] = 0.0f;
-    const v4i bias = {MMQ_BIAS, MMQ_BIAS, MMQ_BIAS, MMQ_BIAS};
+    const v4i_v1 bias = {MMQ_V1_BIAS, MMQ_V1_BIAS, MMQ_V1_BIAS, MMQ_V1_BIAS};
 
-    // Block scales straight from the staged images, per lane: the f16 bits of d_w (and m_w) of the
-    // 4 weight rows 16 i + 4 q + e it accumulates (used as f16 by v_fma_mix_f32, no convert), and
-    // {d_a, -d_a * 1.5*2^23, -c * s_a} of its token 16 t + r16 with c = 8 (Q4_0), 16 (Q5_0),
-    // 0 (Q8_0) or -1 (Q4_1 / Q5_1: + m_w * s_a). Only LDS reads in the main loop: an LDS write
-    // there makes hipcc wait for every DMA in flight (vmcnt(0)), which serialised the double buffer.
-    constexpr float CS = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : -1.0f;
-    constexpr bool HAS_M = T::MOFF >= 0;
+    // Block scales straight from the staged images, per lane: d (and m) of the 4 weight rows
+    // 16 i + 4 q + e it accumulates, {d_a, -d_a * 1.5*2^23, c * s_a} of its token 16 t + r16 with
+    // c = 8 (Q4_0), 16 (Q5_0), 0 (Q8_0) or 1 (Q4_1 / Q5_1: m_w * s_a). Only LDS reads in the
+    // main loop: an LDS write there makes hipcc wait for every DMA in flight (vmcnt(0)), which
+    // serialised the double buffer.
+    constexpr float CS = F == FMT_Q4_0 ? 8.0f : F == FMT_Q5_0 ? 16.0f : F == FMT_Q8_0 ? 0.0f : 1.0f;
     struct blk_t {
-        v4i c[G::RT][TT];
-        uint32_t dw[G::RT][4], mw[G::RT][4];
-        f32x2 da[TT], nda[TT], ncs[TT];  // token scalars, duplicated for the packed-f32 ops
+        v4i_v1 c[G::RT][TT];
+        float4 dw[G::RT], mw[G::RT];
+        float4 as[TT];  // {d_a, -d_a * bias, c * s_a, -}
     };
-    auto u16 = [](const uint8_t* p) { return (uint32_t)*reinterpret_cast<const uint16_t*>(p); };
-    // Epilogue, two elements (rows e, e+1 of one token) per packed op:
-    //   Q4_0 / Q5_0 / Q8_0: acc += d_w * (fma(d_a, cf, -d_a*1.5*2^23) - c*s_a)   [pk_fma, pk_add, fma_mix]
-    //   Q4_1 / Q5_1:        acc += (d_w * d_a) * sumi + m_w * s_a   (ncs = +s_a)   [fma_mix, pk_mul, fma_mix, add]
-    // fma(d_a, cf, -d_a*1.5*2^23) = round(d_a * sumi) exactly (cf = 1.5*2^23 + sumi, exact constant).
+    auto h16 = [](const uint8_t* p) { return h2f(*reinterpret_cast<const uint16_t*>(p)); };
     auto epilogue = [&](const blk_t& p, int h, int b) {
 #pragma unroll
         for (int t = 0; t < TT; ++t)
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
-                if constexpr (SUMI) {
+                const float dws[4] = {p.dw[i].x, p.dw[i].y, p.dw[i].z, p.dw[i].w};
+                const float mws[4] = {p.mw[i].x, p.mw[i].y, p.mw[i].z, p.mw[i].w};
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < 4; ++e) {
+                    const int ce = p.c[i][t][e];
+                    if constexpr (SUMI) {
                         const int n = n0 + 16 * i + 4 * q + e, m = m0 + 16 * t + r16;
-                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * MMQ_SB + b] = p.c[i][t][e] - MMQ_BIAS;
-                    }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; e += 2) {
-                        const f32x2 cf = {__int_as_float(p.c[i][t][e]), __int_as_float(p.c[i][t][e + 1])};
-                        float* a = &acc[(i * TT + t) * 4 + e];
-                        if constexpr (!HAS_M) {
-                            f32x2 t2 = __builtin_elementwise_fma(p.da[t], cf, p.nda[t]);  // d_a * sumi
-                            if constexpr (CS != 0.0f) t2 = t2 + p.ncs[t];                   // - c * s_a
-                            a[0] = fma_mix_lo(p.dw[i][e], t2.x, a[0]);
-                            a[1] = fma_mix_lo(p.dw[i][e + 1], t2.y, a[1]);
+                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * MMQ_V1_SB + b] = ce - MMQ_V1_BIAS;
+                    } else {
+                        const float cf = __int_as_float(ce);  // = 1.5*2^23 + sumi, exact
+                        float& a = acc[(i * TT + t) * 4 + e];
+                        if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0 || F == FMT_Q8_0) {
+                            const float t1 = __builtin_fmaf(p.as[t].x, cf, p.as[t].y);  // round(d_a * sumi)
+                            const float t2 = t1 - p.as[t].z;                          // - 8 s_a / - 16 s_a / - 0
+                            a = __builtin_fmaf(dws[e], t2, a);
                         } else {
-                            const f32x2 x = cf - f32x2{MMQ_BIAS_F, MMQ_BIAS_F};            // exact: sumi
-                            const f32x2 dd = {fma_mix_lo(p.dw[i][e], p.da[t].x, -0.0f),
-                                              fma_mix_lo(p.dw[i][e + 1], p.da[t].x, -0.0f)};  // d_w * d_a
-                            const f32x2 t1 = dd * x;
-                            const f32x2 tm = {fma_mix_lo(p.mw[i][e], p.ncs[t].x, t1.x),
-                                              fma_mix_lo(p.mw[i][e + 1], p.ncs[t].x, t1.y)};  // + m_w * s_a
-                            a[0] += tm.x;
-                            a[1] += tm.y;
+                            const float x = cf - MMQ_V1_BIAS_F;                          // exact: = sumi
+                            const float t1 = dws[e] * p.as[t].x * x;                  // (d_w * d_a) * fs
+                            a += __builtin_fmaf(mws[e], p.as[t].z, t1);
                         }
                     }
                 }
@@ -259,9 +208,9 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     // the later blocks' MFMAs and epilogues, plus an explicit wait for the matrix pipe: reading
     // them with only the wait states hipcc inserts gave wrong sums, tools/mmq_debug.hip).
     auto compute = [&](uint8_t* buf, int h, int sh) {
-        blk_t blk[MMQ_SB];
-        long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
-        static_for<MMQ_SB>([&](auto BI) {
+        blk_t blk[MMQ_V1_SB];
+        long afrag[MMQ_V1_SB][G::RT], bfrag[MMQ_V1_SB][TT];
+        static_for<MMQ_V1_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
             constexpr int o = b * T::BB;
 #pragma unroll
@@ -269,25 +218,25 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
                 uint32_t lo, hi;
                 if constexpr (T::Q8) {  // signed bytes, elements 4q.. and 16+4q..
-                    lo = lds32<o + T::QS>(wr + 4 * q);
-                    hi = lds32<o + T::QS + 16>(wr + 4 * q);
+                    lo = lds32_v1<o + T::QS>(wr + 4 * q);
+                    hi = lds32_v1<o + T::QS + 16>(wr + 4 * q);
                 } else {
-                    const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
+                    const uint32_t v = lds32_v1<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
                     lo = v & 0x0F0F0F0Fu;
                     hi = (v >> 4) & 0x0F0F0F0Fu;
                 }
                 if constexpr (T::QH >= 0) {
-                    const uint32_t qh = lds32<o + T::QH>(wr);
+                    const uint32_t qh = lds32_v1<o + T::QH>(wr);
                     lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
                     hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
                 }
                 afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
                 const uint8_t* sr = buf + (16 * i + 4 * q) * G::RIMG + sh + o;  // rows 16 i + 4 q + e
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    blk[b].dw[i][e] = u16(sr + e * G::RIMG);
-                    if constexpr (HAS_M) blk[b].mw[i][e] = u16(sr + e * G::RIMG + T::MOFF);
-                }
+                blk[b].dw[i] = make_float4(h16(sr), h16(sr + G::RIMG), h16(sr + 2 * G::RIMG), h16(sr + 3 * G::RIMG));
+                if constexpr (T::MOFF >= 0)
+                    blk[b].mw[i] = make_float4(h16(sr + T::MOFF), h16(sr + G::RIMG + T::MOFF),
+                                               h16(sr + 2 * G::RIMG + T::MOFF), h16(sr + 3 * G::RIMG + T::MOFF));
+                else blk[b].mw[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
@@ -297,14 +246,11 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
                 bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
                 const uint32_t dsh = *reinterpret_cast<const uint32_t*>(ar);
                 const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
-                const float nda = -(da * MMQ_BIAS_F), ncs = -(CS * sa);
-                blk[b].da[t] = f32x2{da, da};
-                blk[b].nda[t] = f32x2{nda, nda};
-                blk[b].ncs[t] = f32x2{ncs, ncs};
+                blk[b].as[t] = make_float4(da, -(da * MMQ_V1_BIAS_F), CS * sa, 0.0f);
             }
         });
         __builtin_amdgcn_sched_barrier(0);
-        static_for<MMQ_SB>([&](auto BI) {
+        static_for<MMQ_V1_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
 #pragma unroll
             for (int t = 0; t < TT; ++t)
@@ -315,29 +261,29 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
+        static_for<MMQ_V1_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // this wave's stages h = wave + k W, k < nst; up to NB of them in flight
-    const int nst = wave < H ? (H - 1 - wave) / W + 1 : 0;
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-        if (k < nst) issue(wave + k * W, bufs + k * G::BUF);
-    for (int k = 0; k < nst; ++k) {
-        const int h = wave + k * W;
-        uint8_t* cur = bufs + (k % NB) * G::BUF;
-        wait_stage<G::NI>(min(nst - 1 - k, NB - 1));  // this stage's DMA landed
+    int k = 0;
+    if (wave < H) issue(wave, bufs);
+    for (int h = wave; h < H; h += W, ++k) {
+        uint8_t* cur = bufs + (k & 1) * G::BUF;
+        if (h + W < H) {
+            issue(h + W, bufs + ((k + 1) & 1) * G::BUF);   // next stage in flight during this one
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NI) : "memory");  // this stage's DMA landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
 #ifdef QG_MMQ_STAMPS
-        if (k == 0) MMQ_STAMP(1);
+        if (h == wave) MMQ_V1_STAMP(1);
 #endif
         compute(cur, h, G::shift(h));
 #ifdef QG_MMQ_STAMPS
-        if (k == 0) MMQ_STAMP(2);
+        if (h == wave) MMQ_V1_STAMP(2);
 #endif
-        if (k + NB < nst) issue(h + NB * W, cur);  // refill the buffer just consumed
     }
-    MMQ_STAMP(3);
+    MMQ_V1_STAMP(3);
 
     if constexpr (!SUMI) {
         // fixed-order sum of the W partial tiles, in the wave buffers once every wave is done
@@ -358,21 +304,21 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
         }
     }
 #ifdef QG_MMQ_STAMPS
-    MMQ_STAMP(4);
+    MMQ_V1_STAMP(4);
     if (lane == 0) {
         const int wv = (blockIdx.y * gridDim.x + blockIdx.x) * W + wave;
-        for (int kk = 0; kk < 5; ++kk) g_mmq_stamps[8 * wv + kk] = stamps[kk];
+        for (int kk = 0; kk < 5; ++kk) g_mmq_v1_stamps[8 * wv + kk] = stamps[kk];
     }
 #endif
 }
 
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
 // rows and stages aligned to the DMA piece, 32-bit byte offsets. P16 additionally: a 16-B aligned B
-// and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_geom).
-template <int F, int BN, int TT, int W, bool P16, int NB = 2>
-inline bool mmq_shape_ok(const GemmArgs& g) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
-    if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_SB) != 0) return false;
+// and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_v1_geom).
+template <int F, int BN, int TT, int W, bool P16>
+inline bool mmq_v1_shape_ok(const GemmArgs& g) {
+    using G = mmq_v1_geom<F, BN, TT, W, P16>;
+    if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_V1_SB) != 0) return false;
     const long RB = (long)(g.K / QK) * wfmt<F>::BB, AB = (long)(g.K / QK) * Q8_1_BYTES;
     if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
     if (P16 && G::RSB % 16 != 0 && g.K % 256 != 0) return false;
@@ -381,11 +327,11 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2>
-hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
+template <int F, int BN, int TT, int W, bool SUMI, bool P16>
+hipError_t mmq_v1_launch(const GemmArgs& g, hipStream_t st) {
+    using G = mmq_v1_geom<F, BN, TT, W, P16>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB>;
+    auto k = mmq_v1_kernel<F, BN, TT, W, SUMI, P16>;
     if (G::LDS > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {
