@@ -122,10 +122,21 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # QG_BENCH_BACKEND=gloo with ranks sharing a device: a rehearsal of the N>1 code path on a
+    # one-GPU box (the real multi-GPU run is one rank per GPU over RCCL)
+    backend = os.environ.get("QG_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        # communicator set-up outside every measured region (even with --warmup 0)
+        probe = torch.zeros(world, device=dev)
+        dist.all_gather_into_tensor(probe, probe[rank:rank + 1].clone())
+        dist.barrier()
 
     wtype = WTYPES[args.wtype]
     bb = qg.BLOCK_BYTES[wtype]
