@@ -126,7 +126,9 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NI) : "memory");
 }
 
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2>
+// ABL (tuning probes only; the product uses 0): 1 = the DMA stream and waits without any compute,
+// 2 = operand reads + MFMAs without the VALU epilogue.
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n) {
@@ -315,27 +317,44 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
+        if constexpr (ABL == 2) {
+            static_for<MMQ_SB>([&](auto BI) {
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) acc[(i * TT + t) * 4] += __int_as_float(blk[decltype(BI)::value].c[i][t][0]);
+            });
+        } else {
+            static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
+        }
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // this wave's stages h = wave + k W, k < nst; up to NB of them in flight
+    // this wave's stages h = wave + k W (k < nst), up to NB of them in flight. ROT: the workgroups
+    // of one XCD (blockIdx.x = c mod 8) start at different rounds of W stages, so they do not all
+    // pull the same activation lines through their L2 at the same moment; each wave keeps its set
+    // of stages (rotation by a multiple of W when W divides H), only their order changes.
     const int nst = wave < H ? (H - 1 - wave) / W + 1 : 0;
+    const int rot = ROT && H % W == 0 ? (int)(((blockIdx.x >> 3) * W) % H) : 0;
+    auto stage = [&](int k) {
+        const int h = wave + rot + k * W;
+        return h >= H ? h - H : h;
+    };
 #pragma unroll
     for (int k = 0; k < NB; ++k)
-        if (k < nst) issue(wave + k * W, bufs + k * G::BUF);
+        if (k < nst) issue(stage(k), bufs + k * G::BUF);
     for (int k = 0; k < nst; ++k) {
-        const int h = wave + k * W;
+        const int h = stage(k);
         uint8_t* cur = bufs + (k % NB) * G::BUF;
         wait_stage<G::NI>(min(nst - 1 - k, NB - 1));  // this stage's DMA landed
 #ifdef QG_MMQ_STAMPS
         if (k == 0) MMQ_STAMP(1);
 #endif
-        compute(cur, h, G::shift(h));
+        if constexpr (ABL != 1) compute(cur, h, G::shift(h));
 #ifdef QG_MMQ_STAMPS
         if (k == 0) MMQ_STAMP(2);
 #endif
-        if (k + NB < nst) issue(h + NB * W, cur);  // refill the buffer just consumed
+        if (k + NB < nst) issue(stage(k + NB), cur);  // refill the buffer just consumed
     }
     MMQ_STAMP(3);
 
@@ -381,11 +400,11 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     using G = mmq_geom<F, BN, TT, W, P16, NB>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT>;
     if (G::LDS > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {

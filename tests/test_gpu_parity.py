@@ -105,6 +105,38 @@ def test_sumi_bit_exact(O, qg, t, algo, m, n, k):
     assert np.array_equal(got, want)
 
 
+def random_byte_case(m, n, k, t, seed=7):
+    """Raw random blocks: every weight nibble / byte value and every activation byte including
+    -128 (which no quantizer emits), with finite f16 scales — the integer paths' full input range."""
+    rng = np.random.default_rng(seed)
+    nb, bb = k // 32, {2: 18, 3: 20, 6: 22, 7: 24, 8: 34}[t]
+    aq = rng.integers(0, 256, (m, nb, 36), dtype=np.uint8)
+    bq = rng.integers(0, 256, (n, nb, bb), dtype=np.uint8)
+    f16 = lambda lo, hi, shape: rng.uniform(lo, hi, shape).astype(np.float16).view(np.uint8).reshape(shape + (2,))
+    aq[..., 0:2] = f16(1e-3, 2e-2, (m, nb))
+    aq[..., 2:4] = f16(-5.0, 5.0, (m, nb))
+    bq[..., 0:2] = f16(-0.1, 0.1, (n, nb))
+    if t in (3, 7):
+        bq[..., 2:4] = f16(-0.5, 0.5, (n, nb))
+    aq[0, 0, 4:36] = 0x80            # a whole block of -128
+    bq[0, 0, bb - 16:] = 0x00 if t != 8 else 0x80   # nibbles 0 (q - 8 = -8) / bytes -128
+    return aq, bq
+
+
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("algo", ["gemv", "mfma", "generic"])
+@pytest.mark.parametrize("m,n,k", [(1, 96, 4096), (4, 33, 1024), (24, 48, 2048)])
+def test_random_bytes_bit_exact(O, qg, t, algo, m, n, k):
+    if algo == "gemv" and m > 8:
+        pytest.skip("GEMV path is M <= 8")
+    aq, bq = random_byte_case(m, n, k, t)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t, ALGOS[algo]))
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=ALGOS[algo]))
+    assert_close_to_oracle(O, c, aq, bq, t)
+
+
 # ------------------------------------------------------------------------------- outputs
 @pytest.mark.parametrize("t", WTYPES)
 @pytest.mark.parametrize("m", [1, 2, 3, 4, 5, 8])

@@ -159,10 +159,10 @@ static void add_read(std::vector<Variant>& vs, Problem& p) {
 template <int F> static void m1(std::vector<Variant>& vs, bool full) {
     V1(F, 1, 4, 32, 512, "v1 bpl4 lpr32 wg512")
     STAGED(F, 1, 4, 32, 512, "v2 bpl4 lpr32 wg512")
-    STAGED_NT(F, 1, 4, 32, 512, "v2 nt bpl4 lpr32 wg512")
-    STAGED(F, 1, 4, 16, 512, "v2 bpl4 lpr16 wg512")
+    STAGED(F, 1, 2, 64, 1024, "v2 bpl2 lpr64 wg1024")
+    STAGED(F, 1, 2, 64, 512, "v2 bpl2 lpr64 wg512")
+    STAGED(F, 1, 2, 32, 512, "v2 bpl2 lpr32 wg512")
     STAGED(F, 1, 4, 32, 256, "v2 bpl4 lpr32 wg256")
-    STAGED_NT(F, 1, 4, 32, 256, "v2 nt bpl4 lpr32 wg256")
     if (full) {
         RAX(F, 1, 4, 32, 128, false, "ra bpl4 lpr32 wg128")
         RAX(F, 1, 4, 32, 512, false, "ra bpl4 lpr32 wg512")

@@ -72,17 +72,24 @@ int main() {
 #define VN(BN, TT, W, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB>(g, st) : hipErrorInvalidValue; }});
         VN(32, 1, 8, 2, "v2 bn32 tt1 w8 nb2")
-        VN(32, 1, 8, 3, "v2 bn32 tt1 w8 nb3")
-        VN(32, 1, 8, 4, "v2 bn32 tt1 w8 nb4")
-        VN(16, 1, 8, 4, "v2 bn16 tt1 w8 nb4")
         VN(16, 2, 8, 2, "v2 bn16 tt2 w8 nb2")
-        VN(16, 2, 8, 3, "v2 bn16 tt2 w8 nb3")
-        VN(32, 1, 4, 4, "v2 bn32 tt1 w4 nb4")
-        VN(32, 2, 8, 2, "v2 bn32 tt2 w8 nb2")
         VN(32, 2, 4, 2, "v2 bn32 tt2 w4 nb2")
-        VN(32, 2, 4, 3, "v2 bn32 tt2 w4 nb3")
-        VN(32, 2, 4, 4, "v2 bn32 tt2 w4 nb4")
-        VN(16, 4, 4, 3, "v2 bn16 tt4 w4 nb3")
+#define VA(BN, TT, W, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, 2>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, 2, ABL>(g, st) : hipErrorInvalidValue; }});
+        VA(32, 1, 8, 1, "abl1 loads bn32 tt1 w8")
+        VA(32, 1, 8, 2, "abl2 no-epi bn32 tt1 w8")
+        VA(16, 1, 8, 1, "abl1 loads bn16 tt1 w8")
+        VA(32, 2, 4, 1, "abl1 loads bn32 tt2 w4")
+#define VR(BN, TT, W, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, 2>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, 2, ABL, true>(g, st) : hipErrorInvalidValue; }});
+        VR(32, 1, 8, 0, "rot bn32 tt1 w8")
+        VR(32, 1, 8, 1, "rot abl1 loads bn32 tt1 w8")
+        VR(16, 1, 8, 0, "rot bn16 tt1 w8")
+        VR(16, 2, 8, 0, "rot bn16 tt2 w8")
+        VR(32, 2, 8, 0, "rot bn32 tt2 w8")
+        VR(32, 2, 4, 0, "rot bn32 tt2 w4")
+#undef VR
+#undef VA
 #undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
