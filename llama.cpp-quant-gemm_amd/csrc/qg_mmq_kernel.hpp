@@ -127,7 +127,8 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 }
 
 // ABL (tuning probes only; the product uses 0): 1 = the DMA stream and waits without any compute,
-// 2 = operand reads + MFMAs without the VALU epilogue.
+// 2 = operand reads + MFMAs without the VALU epilogue, 3 / 4 = as 1 with only the activation /
+// only the weight pieces fetched (the other lanes re-read a line already in flight).
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
@@ -172,6 +173,8 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
             const int p = min(64 * i + lane, G::WPC + G::APC - 1);
             cisw[i] = p < G::WPC;
             coff[i] = cisw[i] ? wpiece(p) : apiece(p - G::WPC);
+            if constexpr (ABL == 3) if (cisw[i]) { cisw[i] = false; coff[i] = apiece(min(p, G::APC - 1)); }
+            if constexpr (ABL == 4) if (!cisw[i]) { cisw[i] = true; coff[i] = wpiece(0); }
         }
     } else {
 #pragma unroll
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #ifdef QG_MMQ_STAMPS
         if (k == 0) MMQ_STAMP(1);
 #endif
-        if constexpr (ABL != 1) compute(cur, h, G::shift(h));
+        if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(cur, h, G::shift(h));
 #ifdef QG_MMQ_STAMPS
         if (k == 0) MMQ_STAMP(2);
 #endif

@@ -15,7 +15,8 @@
 #include <vector>
 
 #include "qg_mmq_kernel.hpp"
-#include "mmq_v1.hpp"  // round-1 product kernel (A/B baseline)
+#include "mmq_v1.hpp"
+#include "mmq_tile_experiment.hpp"  // measured slower than the product, kept for the record  // round-1 product kernel (A/B baseline)
 #include "../include/qg/qg.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -80,16 +81,23 @@ int main() {
         VA(32, 1, 8, 2, "abl2 no-epi bn32 tt1 w8")
         VA(16, 1, 8, 1, "abl1 loads bn16 tt1 w8")
         VA(32, 2, 4, 1, "abl1 loads bn32 tt2 w4")
-#define VR(BN, TT, W, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, 2>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, 2, ABL, true>(g, st) : hipErrorInvalidValue; }});
-        VR(32, 1, 8, 0, "rot bn32 tt1 w8")
-        VR(32, 1, 8, 1, "rot abl1 loads bn32 tt1 w8")
-        VR(16, 1, 8, 0, "rot bn16 tt1 w8")
-        VR(16, 2, 8, 0, "rot bn16 tt2 w8")
-        VR(32, 2, 8, 0, "rot bn32 tt2 w8")
-        VR(32, 2, 4, 0, "rot bn32 tt2 w4")
-#undef VR
+        VA(32, 1, 8, 3, "abl3 act-only bn32 tt1 w8")
+        VA(32, 1, 8, 4, "abl4 wt-only bn32 tt1 w8")
+        VA(16, 2, 8, 1, "abl1 loads bn16 tt2 w8")
+        VA(16, 2, 8, 3, "abl3 act-only bn16 tt2 w8")
+        VA(16, 2, 8, 4, "abl4 wt-only bn16 tt2 w8")
 #undef VA
+#define VT(WR, WT, RT, TT, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_tile_shape_ok<FMT_Q4_0, WR, WT, RT, TT, NB>(g) ? mmq_tile_launch<FMT_Q4_0, WR, WT, RT, TT, NB, false>(g, st) : hipErrorInvalidValue; }});
+        VT(4, 2, 2, 2, 2, "tile 128x64 w8 nb2")
+        VT(4, 2, 2, 2, 3, "tile 128x64 w8 nb3")
+        VT(2, 2, 2, 2, 2, "tile 64x64 w4 nb2")
+        VT(2, 2, 2, 2, 3, "tile 64x64 w4 nb3")
+        VT(4, 1, 2, 2, 2, "tile 128x32 w4 nb2")
+        VT(2, 2, 2, 1, 2, "tile 64x32 w4 nb2")
+        VT(4, 2, 1, 2, 2, "tile 64x64 w8 nb2")
+        VT(2, 4, 2, 1, 2, "tile 64x64 w8b nb2")
+#undef VT
 #undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
