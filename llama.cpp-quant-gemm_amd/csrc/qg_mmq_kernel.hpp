@@ -49,7 +49,7 @@ __device__ __forceinline__ float fma_mix_lo(uint32_t h, float x, float c) {
 
 constexpr int MMQ_BIAS = 0x4B400000;  // bits of 12582912.0f = 1.5 * 2^23
 constexpr float MMQ_BIAS_F = 12582912.0f;
-constexpr int MMQ_SB = 4;             // blocks per stage
+constexpr int MMQ_SB = 4;             // blocks per compute sub-stage (a DMA stage holds SB = 4 or 8)
 
 #ifdef QG_MMQ_STAMPS
 // diagnostic build only (tools/mmq_timeline.hip): per-wave s_memrealtime stamps
@@ -89,15 +89,22 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // one stage in flight ahead of the one being computed).
 // With 16-B weight pieces the weight and activation pieces of a stage share one piece numbering
 // (p < WPC: weights, then activations), so only the last DMA instruction carries padding.
-template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2> struct mmq_geom {
+// SB: blocks per stage (4 or 8). With 8, every format's stage segment is a 16-B multiple (no
+// shifted windows) and each token's activation segment is 288 B (+16 B pad against 2-way LDS bank
+// conflicts).
+template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4> struct mmq_geom {
     using T = wfmt<F>;
-    static constexpr int RSB = MMQ_SB * T::BB;                // weight bytes per row per stage
+    static_assert(SB == 4 || SB == 8, "4 or 8 blocks per stage");
+    static constexpr int RSB = SB * T::BB;                     // weight bytes per row per stage
     static constexpr int WPS = P16 ? 16 : 4;                   // weight DMA piece (bytes)
     static constexpr int RIMG = P16 && RSB % 16 != 0 ? RSB + 8 : RSB;  // row image bytes
     static constexpr int PPR = RIMG / WPS;                     // pieces per row image
     static constexpr int WPC = BN * PPR;                       // weight pieces per stage
     static constexpr int NTOK = 16 * TT;
-    static constexpr int APC = NTOK * 9;                       // activation 16-B pieces per stage
+    static constexpr int APR = 9 * SB / 4;                     // activation 16-B pieces per token
+    static constexpr int APT = SB == 4 ? APR : APR + 1;        // ... incl. the pad piece
+    static constexpr int ASTR = APT * 16;                      // token image stride (bytes)
+    static constexpr int APC = NTOK * APT;                     // activation 16-B pieces per stage
     static constexpr bool CMB = P16;                           // combined piece numbering
     static constexpr int NWI = CMB ? 0 : (WPC + 63) / 64;      // weight-only DMA instructions
     static constexpr int NAI = CMB ? 0 : (APC + 63) / 64;      // activation-only DMA instructions
@@ -129,11 +136,11 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // ABL (tuning probes only; the product uses 0): 1 = the DMA stream and waits without any compute,
 // 2 = operand reads + MFMAs without the VALU epilogue, 3 / 4 = as 1 with only the activation /
 // only the weight pieces fetched (the other lanes re-read a line already in flight).
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
     using T = wfmt<F>;
     static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * G::NTOK;
     const int nb = K / QK;
-    const int H = nb / MMQ_SB;  // stages
+    const int H = nb / SB;  // stages
     const long RB = (long)nb * T::BB;
     const long AB = (long)nb * Q8_1_BYTES;
     uint8_t* bufs = smem + wave * NB * G::BUF;
@@ -161,8 +168,8 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
         return (int)((long)min(n0 + row, N - 1) * RB) + (p - row * G::PPR) * G::WPS;
     };
     auto apiece = [&](int p) {  // activation piece p of a stage: byte offset in A
-        const int tok = p / 9;
-        return (int)((long)min(m0 + tok, M - 1) * AB) + (p - tok * 9) * 16;
+        const int tok = p / G::APT;
+        return (int)((long)min(m0 + tok, M - 1) * AB) + min(p - tok * G::APT, G::APR - 1) * 16;
     };
     constexpr int NOFF = G::CMB ? G::NI : 1;
     int woff[G::CMB ? 1 : G::NWI], aoff[G::CMB ? 1 : G::NAI], coff[NOFF];
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     // (found by tools/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = B + (long)h * G::RSB - G::shift(h);
-        const uint8_t* asrc = A + (long)h * 144;
+        const uint8_t* asrc = A + (long)h * (SB * Q8_1_BYTES);
         if constexpr (G::CMB) {
 #pragma unroll
             for (int i = 0; i < G::NI; ++i) glds<16>((cisw[i] ? wsrc : asrc) + coff[i], buf + 64 * i * 16);
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int n = n0 + 16 * i + 4 * q + e, m = m0 + 16 * t + r16;
-                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * MMQ_SB + b] = p.c[i][t][e] - MMQ_BIAS;
+                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * SB + b] = p.c[i][t][e] - MMQ_BIAS;
                     }
                 } else {
 #pragma unroll
@@ -263,12 +270,13 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     // 4 x RT x TT MFMAs back to back, then the VALU epilogues (block b's results are read behind
     // the later blocks' MFMAs and epilogues, plus an explicit wait for the matrix pipe: reading
     // them with only the wait states hipcc inserts gave wrong sums, tools/mmq_debug.hip).
-    auto compute = [&](uint8_t* buf, int h, int sh) {
+    auto compute4 = [&](uint8_t* buf, int h, int sh, auto SUB) {
+        constexpr int b0 = 4 * decltype(SUB)::value;  // first block of this 4-block sub-stage
         blk_t blk[MMQ_SB];
         long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
         static_for<MMQ_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
-            constexpr int o = b * T::BB;
+            constexpr int o = (b0 + b) * T::BB;
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
             }
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * 144 + b * Q8_1_BYTES;
+                const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * G::ASTR + (b0 + b) * Q8_1_BYTES;
                 const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
                 const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
                 bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
@@ -328,9 +336,13 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
                     for (int t = 0; t < TT; ++t) acc[(i * TT + t) * 4] += __int_as_float(blk[decltype(BI)::value].c[i][t][0]);
             });
         } else {
-            static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, decltype(BI)::value); });
+            static_for<MMQ_SB>([&](auto BI) { epilogue(blk[decltype(BI)::value], h, b0 + decltype(BI)::value); });
         }
         __builtin_amdgcn_sched_barrier(0);
+    };
+
+    auto compute = [&](uint8_t* buf, int h, int sh) {
+        static_for<SB / 4>([&](auto SUB) { compute4(buf, h, sh, SUB); });
     };
 
     // this wave's stages h = wave + k W (k < nst), up to NB of them in flight. ROT: the workgroups
@@ -391,10 +403,10 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
 // rows and stages aligned to the DMA piece, 32-bit byte offsets. P16 additionally: a 16-B aligned B
 // and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_geom).
-template <int F, int BN, int TT, int W, bool P16, int NB = 2>
+template <int F, int BN, int TT, int W, bool P16, int NB = 2, int SB = 4>
 inline bool mmq_shape_ok(const GemmArgs& g) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
-    if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_SB) != 0) return false;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
+    if (g.M < 1 || g.N < 1 || g.K % (QK * SB) != 0) return false;
     const long RB = (long)(g.K / QK) * wfmt<F>::BB, AB = (long)(g.K / QK) * Q8_1_BYTES;
     if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
     if (P16 && G::RSB % 16 != 0 && g.K % 256 != 0) return false;
@@ -403,11 +415,11 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB>;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB>;
     if (G::LDS > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {

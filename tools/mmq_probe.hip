@@ -87,17 +87,15 @@ int main() {
         VA(16, 2, 8, 3, "abl3 act-only bn16 tt2 w8")
         VA(16, 2, 8, 4, "abl4 wt-only bn16 tt2 w8")
 #undef VA
-#define VT(WR, WT, RT, TT, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        return g.wtype == FMT_Q4_0 && mmq_tile_shape_ok<FMT_Q4_0, WR, WT, RT, TT, NB>(g) ? mmq_tile_launch<FMT_Q4_0, WR, WT, RT, TT, NB, false>(g, st) : hipErrorInvalidValue; }});
-        VT(4, 2, 2, 2, 2, "tile 128x64 w8 nb2")
-        VT(4, 2, 2, 2, 3, "tile 128x64 w8 nb3")
-        VT(2, 2, 2, 2, 2, "tile 64x64 w4 nb2")
-        VT(2, 2, 2, 2, 3, "tile 64x64 w4 nb3")
-        VT(4, 1, 2, 2, 2, "tile 128x32 w4 nb2")
-        VT(2, 2, 2, 1, 2, "tile 64x32 w4 nb2")
-        VT(4, 2, 1, 2, 2, "tile 64x64 w8 nb2")
-        VT(2, 4, 2, 1, 2, "tile 64x64 w8b nb2")
-#undef VT
+#define VS(BN, TT, W, NB, SB, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB, SB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB, ABL, false, SB>(g, st) : hipErrorInvalidValue; }});
+        VS(32, 1, 8, 2, 8, 0, "sb8 bn32 tt1 w8 nb2")
+        VS(32, 1, 8, 2, 8, 1, "sb8 abl1 loads bn32 tt1 w8")
+        VS(32, 1, 4, 2, 8, 0, "sb8 bn32 tt1 w4 nb2")
+        VS(32, 1, 4, 3, 8, 0, "sb8 bn32 tt1 w4 nb3")
+        VS(16, 1, 8, 2, 8, 0, "sb8 bn16 tt1 w8 nb2")
+        VS(32, 2, 4, 2, 8, 0, "sb8 bn32 tt2 w4 nb2")
+#undef VS
 #undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
