@@ -12,6 +12,12 @@ namespace {
 template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK;
+    // single-row products on long rows or many rows: 2-block units, one row per wave
+    // (profiles/r01_tuning/gemv_probe_v2b.txt: N=32000 -3.4 %, K=14336 -3.8 %)
+    if (MT == 1 && !SUMI && nb % 2 == 0 && nb / 2 >= 64) {
+        if (g.K >= 8192) return gemv_launch<F, 1, 2, 64, 1024, SUMI, AIN>(g, st);
+        if (g.N >= 16384) return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
+    }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);
         return gemv_launch<F, MT, 4, 4, 256, SUMI, AIN>(g, st);
