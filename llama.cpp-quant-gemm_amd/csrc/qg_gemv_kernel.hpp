@@ -46,6 +46,35 @@
 
 namespace qg {
 
+#ifdef QG_STAMPS
+// diagnostic build only (tools/timeline_probe.hip; never in the product build): per wave 8 slots: 100-MHz stamps at entry,
+// after the activation barrier, weights landed, compute done, exit; s_memtime at entry and exit;
+// (XCC_ID << 32 | HW_ID)
+__device__ unsigned long long g_stamps[8 * 65536];
+#define QG_STAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define QG_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define QG_STAMP_STORE(...)                                                                       \
+    do {                                                                                          \
+        if ((threadIdx.x & 63) == 0) {                                                            \
+            unsigned hw, xcc;                                                                     \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));                      \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                    \
+            const int wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                   \
+            const unsigned long long vals[7] = {__VA_ARGS__};                                     \
+            for (int q = 0; q < 7; ++q) g_stamps[8 * wv + q] = vals[q];                           \
+            g_stamps[8 * wv + 7] = ((unsigned long long)xcc << 32) | hw;                          \
+        }                                                                                         \
+    } while (0)
+#define QG_WAIT_STAMP(v)                                                                          \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                              \
+    unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define QG_STAMP(v)
+#define QG_CLK(v)
+#define QG_STAMP_STORE(...)
+#define QG_WAIT_STAMP(v)
+#endif
+
 constexpr uint32_t ACC_BIAS = 0x4B400000u;  // bits of 12582912.0f = 1.5 * 2^23
 constexpr float ACC_BIAS_F = 12582912.0f;
 
@@ -183,6 +212,8 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
                                                    float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                    int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
     using G = gemv_geom<F, BPL>;
+    QG_STAMP(t0);
+    QG_CLK(c0);
     A = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A) + blockIdx.y * sA);
     B += blockIdx.y * sB;
     C += blockIdx.y * sC;
@@ -250,6 +281,8 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
         }
     }
     __syncthreads();
+    QG_STAMP(tb);
+    QG_WAIT_STAMP(t1);
 
     float acc[MT];
 #pragma unroll
@@ -285,6 +318,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
             for (int v = 0; v < G::UDW; ++v) cur[v] = nxt[v];
         }
     }
+    QG_STAMP(tc);
     if constexpr (!SUMI) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<LPR>(acc[m]);
@@ -294,6 +328,9 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
                 if (m < M) C[m * ldc_m + row * ldc_n] = acc[m];
         }
     }
+    QG_STAMP(t2);
+    QG_CLK(c2);
+    QG_STAMP_STORE(t0, tb, t1, tc, t2, c0, c2);
 }
 
 // Host side -------------------------------------------------------------------------------------

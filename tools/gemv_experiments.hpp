@@ -6,34 +6,7 @@
 
 namespace qg {
 
-#ifdef QG_STAMPS
-// diagnostic build only (tools/timeline_probe.hip): per wave 8 slots: 100-MHz stamps at entry,
-// after the activation barrier, weights landed, compute done, exit; s_memtime at entry and exit;
-// (XCC_ID << 32 | HW_ID)
-__device__ unsigned long long g_stamps[8 * 65536];
-#define QG_STAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
-#define QG_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
-#define QG_STAMP_STORE(...)                                                                       \
-    do {                                                                                          \
-        if ((threadIdx.x & 63) == 0) {                                                            \
-            unsigned hw, xcc;                                                                     \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));                      \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                    \
-            const int wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                   \
-            const unsigned long long vals[7] = {__VA_ARGS__};                                     \
-            for (int q = 0; q < 7; ++q) g_stamps[8 * wv + q] = vals[q];                           \
-            g_stamps[8 * wv + 7] = ((unsigned long long)xcc << 32) | hw;                          \
-        }                                                                                         \
-    } while (0)
-#define QG_WAIT_STAMP(v)                                                                          \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                              \
-    unsigned long long v = __builtin_amdgcn_s_memrealtime()
-#else
-#define QG_STAMP(v)
-#define QG_CLK(v)
-#define QG_STAMP_STORE(...)
-#define QG_WAIT_STAMP(v)
-#endif
+// QG_STAMPS diagnostics: see qg_gemv_kernel.hpp
 
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned int u32x2b __attribute__((ext_vector_type(2)));

@@ -111,12 +111,10 @@ int main() {
         }
     };
     GemmArgs g; g.A = a; g.C = c; g.M = 1; g.N = N; g.K = K; g.wtype = FMT_Q4_0; g.ldc_m = N; g.ldc_n = 1;
-    auto gemv = [&](const uint8_t* B) { g.B = B; CK((gemv2_launch<FMT_Q4_0, 1, 4, 32, 512, 0, 1>(g, st))); };
-    run("gemv bpl4 lpr32 wg512", 256 * 8, gemv, true);
-    run("gemv bpl4 lpr32 wg512", 256 * 8, gemv, false);
-    auto ra = [&](const uint8_t* B) { g.B = B; CK((gemv_rax_launch<FMT_Q4_0, 4, 32, 256>(g, st))); };
-    run("ra bpl4 lpr32 wg256", 512 * 4, ra, true);
-    run("ra bpl4 lpr32 wg256", 512 * 4, ra, false);
+    // the product kernel (GEMV v2), stamped build
+    auto gemv = [&](const uint8_t* B) { g.B = B; CK((gemv_launch<FMT_Q4_0, 1, 4, 32, 512, false>(g, st))); };
+    run("gemv v2 bpl4 lpr32 wg512", 256 * 8, gemv, true);
+    run("gemv v2 bpl4 lpr32 wg512", 256 * 8, gemv, false);
     const long n16 = wbytes / 16;
     auto rd2 = [&](const uint8_t* B) { hipLaunchKernelGGL(rd_stamp<2>, dim3((unsigned)((n16 / 2 + 255) / 256)), dim3(256), 0, st, B, wbytes, scr); };
     run("read x4 p2 wg256", (int)((n16 / 2 + 255) / 256) * 4, rd2, true);
