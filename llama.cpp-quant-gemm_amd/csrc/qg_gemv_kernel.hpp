@@ -207,7 +207,14 @@ template <int AIN> __device__ __forceinline__ void load_act_block(const uint8_t*
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false>
+// PRE: read the unit's LDS records into registers right after the staging barrier, before the
+// first weight byte is used, so the LDS latency overlaps the weight stream and only VALU work
+// remains once the weights land (MT <= 2: 12 * BPL * MT dwords of registers).
+// ONEU: every lane owns at most one unit (K <= 32 * BPL * LPR): the kernel has no unit loop, so the
+// waits for the weight loads sit at their first use, behind the record reads (with a loop in the
+// kernel, hipcc's wait insertion falls back to vmcnt(0) before the first record read).
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
+          bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                    int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
@@ -288,34 +295,57 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
 
-    const int iters = (U + LPR - 1) / LPR;
-    for (int j = 0; j < iters; ++j) {
-        const int u = lir + j * LPR;
-        uint32_t nxt[G::UDW];
-        if (j + 1 < iters) load_unit(nxt, u + LPR);
-        if (u < U) {
-            static_for<BPL>([&](auto BI) {
-                constexpr int bi = decltype(BI)::value;
+    // one unit of this lane: activation records preloaded (PRE) or read per block
+    auto do_unit = [&](int u) {
+        uint4 pre[PRE ? BPL : 1][PRE ? MT : 1][3];
+        if constexpr (PRE) {
+#pragma unroll
+            for (int bi = 0; bi < BPL; ++bi)
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
-                    if (m < M) {
+                    const uint32_t* rec = lds + (min(m, M - 1) * U + u) * G::REC_DW + bi * 12;
+#pragma unroll
+                    for (int x = 0; x < 3; ++x) pre[bi][m][x] = *reinterpret_cast<const uint4*>(rec + 4 * x);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        static_for<BPL>([&](auto BI) {
+            constexpr int bi = decltype(BI)::value;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                if (m < M) {
+                    uint4 a[3];
+                    if constexpr (PRE) {
+                        a[0] = pre[bi][m][0]; a[1] = pre[bi][m][1]; a[2] = pre[bi][m][2];
+                    } else {
                         const uint32_t* rec = lds + (m * U + u) * G::REC_DW + bi * 12;
-                        const uint4 a[3] = {*reinterpret_cast<const uint4*>(rec),
-                                            *reinterpret_cast<const uint4*>(rec + 4),
-                                            *reinterpret_cast<const uint4*>(rec + 8)};
-                        const uint32_t d = block_dot<F, bi>(cur, a);
-                        if constexpr (SUMI) {
-                            if (row_ok) sumi_out[((long)m * N + row) * nb + u * BPL + bi] = (int)(d - ACC_BIAS);
-                        } else {
-                            acc[m] += block_term_rec<F, bi>(cur, d, a[2]);
-                        }
+                        a[0] = *reinterpret_cast<const uint4*>(rec);
+                        a[1] = *reinterpret_cast<const uint4*>(rec + 4);
+                        a[2] = *reinterpret_cast<const uint4*>(rec + 8);
+                    }
+                    const uint32_t d = block_dot<F, bi>(cur, a);
+                    if constexpr (SUMI) {
+                        if (row_ok) sumi_out[((long)m * N + row) * nb + u * BPL + bi] = (int)(d - ACC_BIAS);
+                    } else {
+                        acc[m] += block_term_rec<F, bi>(cur, d, a[2]);
                     }
                 }
-            });
-        }
-        if (j + 1 < iters) {
+            }
+        });
+    };
+    const int iters = (U + LPR - 1) / LPR;
+    if constexpr (ONEU) {
+        if (lir < U) do_unit(lir);
+    } else {
+        for (int j = 0; j < iters; ++j) {
+            const int u = lir + j * LPR;
+            uint32_t nxt[G::UDW];
+            if (j + 1 < iters) load_unit(nxt, u + LPR);
+            if (u < U) do_unit(u);
+            if (j + 1 < iters) {
 #pragma unroll
-            for (int v = 0; v < G::UDW; ++v) cur[v] = nxt[v];
+                for (int v = 0; v < G::UDW; ++v) cur[v] = nxt[v];
+            }
         }
     }
     QG_STAMP(tc);
@@ -353,12 +383,14 @@ inline bool gemv_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2)>
 hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
-    auto kfn = gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT>;
+    const bool one = g.K / QK / BPL <= LPR;
+    auto kfn = one ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
+                   : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, false>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

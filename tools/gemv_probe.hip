@@ -141,6 +141,8 @@ static void bench(Problem& p, std::vector<Variant>& vs, hipStream_t st, int roun
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false>(g, s); }, false});
 #define STAGED_NT(F, MT, BPL, LPR, WGS, NAME) \
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, true>(g, s); }, false});
+#define NOPRE(F, MT, BPL, LPR, WGS, NAME) \
+    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, false>(g, s); }, false});
 #define V1(F, MT, BPL, LPR, WGS, NAME) \
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_v1_launch<F, MT, BPL, LPR, WGS, 4 * MT, false>(g, s); }, false});
 #define RAX(F, MT, BPL, LPR, WGS, PF, NAME) \
@@ -159,10 +161,10 @@ static void add_read(std::vector<Variant>& vs, Problem& p) {
 template <int F> static void m1(std::vector<Variant>& vs, bool full) {
     V1(F, 1, 4, 32, 512, "v1 bpl4 lpr32 wg512")
     STAGED(F, 1, 4, 32, 512, "v2 bpl4 lpr32 wg512")
-    STAGED(F, 1, 2, 64, 1024, "v2 bpl2 lpr64 wg1024")
-    STAGED(F, 1, 2, 64, 512, "v2 bpl2 lpr64 wg512")
-    STAGED(F, 1, 2, 32, 512, "v2 bpl2 lpr32 wg512")
     STAGED(F, 1, 4, 32, 256, "v2 bpl4 lpr32 wg256")
+    STAGED(F, 1, 2, 64, 512, "v2 bpl2 lpr64 wg512")
+    STAGED(F, 1, 2, 64, 1024, "v2 bpl2 lpr64 wg1024")
+    STAGED(F, 1, 2, 64, 256, "v2 bpl2 lpr64 wg256")
     if (full) {
         RAX(F, 1, 4, 32, 128, false, "ra bpl4 lpr32 wg128")
         RAX(F, 1, 4, 32, 512, false, "ra bpl4 lpr32 wg512")
@@ -183,7 +185,13 @@ int main(int argc, char** argv) {
                         {FMT_Q4_0, 1, 4096, 14336, 3}, {FMT_Q4_0, 1, 14336, 4096, 3}, {FMT_Q4_1, 1, 4096, 4096, 3},
                         {FMT_Q5_0, 1, 4096, 4096, 3}, {FMT_Q5_1, 1, 4096, 4096, 3}, {FMT_Q4_0, 2, 4096, 4096, 3},
                         {FMT_Q4_0, 4, 4096, 4096, 3}, {FMT_Q4_0, 8, 4096, 4096, 3}};
-    for (const S& s : shapes) {
+    const bool focus = getenv("QG_FOCUS") != nullptr;
+    for (const S& s0 : shapes) {
+        S s = s0;
+        if (focus) {
+            if (!(s.F == FMT_Q4_0 && s.M == 1 && s.K == 4096 && (s.N == 4096 || s.N == 4000))) continue;
+            s.rounds = 15;
+        }
         Problem p;
         make(p, s.F, s.M, s.N, s.K, copy);
         std::vector<Variant> vs;
@@ -196,7 +204,8 @@ int main(int argc, char** argv) {
             add_read(vs, p);
         } else if (s.M == 2) {
             V1(FMT_Q4_0, 2, 4, 32, 512, "v1 bpl4 lpr32 wg512")
-            STAGED(FMT_Q4_0, 2, 4, 32, 512, "v2 bpl4 lpr32 wg512")
+            NOPRE(FMT_Q4_0, 2, 4, 32, 512, "v2 nopre bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 2, 4, 32, 512, "v2 pre bpl4 lpr32 wg512")
             STAGED_NT(FMT_Q4_0, 2, 4, 32, 512, "v2 nt bpl4 lpr32 wg512")
             RAX(FMT_Q4_0, 2, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 2, 4, 32, 256, true, "ra bpl4 lpr32 wg256 pf")
