@@ -1,9 +1,9 @@
 // qg_gemv.hip — product instantiations and dispatch of the GEMV kernels (qg_gemv_kernel.hpp).
 //
-// Configuration from the tuning sweeps (tools/gemv_probe.hip, profiles/r01_tuning/): M = 1 with
-// Q4_0/Q4_1: 2-block units, 64 lanes (one wave) per row, 1024-thread workgroups (512 for N >= 16384);
-// otherwise 4-block units (72 B for Q4_0), 32 lanes per row, 512-thread workgroups (one per CU at
-// N=4096); short rows (K/32/4 < 32) 4 lanes per row; K/32 not a multiple of 4: 2-block units.
+// Configuration from the tuning sweeps (tools/gemv_probe.hip, profiles/r01_tuning/): M <= 4 with
+// K >= 4096: 2-block units, 64 lanes (one wave) per row, 1024-thread workgroups (512 for M = 1 and
+// N >= 16384); otherwise 4-block units (72 B for Q4_0), 32 lanes per row, 512-thread workgroups;
+// short rows (K/32/4 < 32) 4 lanes per row; K/32 not a multiple of 4: 2-block units.
 // The fused-quantization variants (AIN_F32 / AIN_F16_FUSED) share the configuration.
 #include "qg_gemv_kernel.hpp"
 
@@ -13,12 +13,17 @@ namespace {
 template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK;
-    // single-row products (nibble-plane formats): 2-block units, one row per wave, records preloaded
-    // (profiles/r01_tuning/gemv_probe_focus.txt: N=K=4096 3.70 -> 3.63 us with 1024-thread
-    // workgroups; gemv_probe_v2b.txt: N=32000 -3.4 % with 512-thread ones, K=14336 -3.8 %)
-    if (MT == 1 && !SUMI && gemv_planes<F> && nb % 2 == 0 && nb / 2 >= 64) {
-        if (g.N >= 16384 && g.K < 8192) return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
-        return gemv_launch<F, 1, 2, 64, 1024, SUMI, AIN>(g, st);
+    // 2-block units, one row per wave, 1024-thread workgroups (512 for a single row of activations
+    // over N >= 16384 rows): profiles/r01_tuning/gemv_probe_focus.txt, gemv_probe_focus2.txt —
+    // M=1 Q4_0 3.67 -> 3.60 us, Q5_0 / Q5_1 -6 %, M=2 -4 %, M=4 -11 % against 4-block units x 32
+    // lanes x 512 threads; gemv_probe_v2b.txt: N=32000 -3.4 %, K=14336 -3.8 %
+    // (a strided batch uses the same shape, so its outputs equal the single launches' bit for bit;
+    // the fused-quantization prologue is repeated per workgroup, so it keeps 16 rows per workgroup,
+    // with the same per-row summation order)
+    if (MT <= 4 && !SUMI && nb % 2 == 0 && nb / 2 >= 64) {
+        if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
+            return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
+        return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN>(g, st);
     }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);

@@ -189,8 +189,8 @@ int main(int argc, char** argv) {
     for (const S& s0 : shapes) {
         S s = s0;
         if (focus) {
-            if (!(s.F == FMT_Q4_0 && s.M == 1 && s.K == 4096 && (s.N == 4096 || s.N == 4000))) continue;
-            s.rounds = 15;
+            if (!(s.K == 4096 && s.N == 4096)) continue;
+            s.rounds = 9;
         }
         Problem p;
         make(p, s.F, s.M, s.N, s.K, copy);
@@ -204,8 +204,9 @@ int main(int argc, char** argv) {
             add_read(vs, p);
         } else if (s.M == 2) {
             V1(FMT_Q4_0, 2, 4, 32, 512, "v1 bpl4 lpr32 wg512")
-            NOPRE(FMT_Q4_0, 2, 4, 32, 512, "v2 nopre bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 2, 4, 32, 512, "v2 pre bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 2, 2, 64, 1024, "v2 pre bpl2 lpr64 wg1024")
+            STAGED(FMT_Q4_0, 2, 2, 64, 512, "v2 pre bpl2 lpr64 wg512")
             STAGED_NT(FMT_Q4_0, 2, 4, 32, 512, "v2 nt bpl4 lpr32 wg512")
             RAX(FMT_Q4_0, 2, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 2, 4, 32, 256, true, "ra bpl4 lpr32 wg256 pf")
@@ -213,6 +214,7 @@ int main(int argc, char** argv) {
         } else if (s.M == 4) {
             V1(FMT_Q4_0, 4, 4, 32, 512, "v1 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 4, 4, 32, 512, "v2 bpl4 lpr32 wg512")
+            STAGED(FMT_Q4_0, 4, 2, 64, 1024, "v2 bpl2 lpr64 wg1024")
             STAGED(FMT_Q4_0, 4, 4, 32, 256, "staged bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 2, 64, 256, false, "ra bpl2 lpr64 wg256")
