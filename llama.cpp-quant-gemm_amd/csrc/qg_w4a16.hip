@@ -358,6 +358,10 @@ hipError_t w16_launch(const GemmArgs& g, hipStream_t st) {
 
 template <int F, int MT> hipError_t w16_launch_mt(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK;
+    // 2-block units, one row per wave, 1024-thread workgroups: half the per-wave work of the 4-block
+    // shape (as the W4A8 GEMV, qg_gemv.hip)
+    if (MT <= 4 && nb % 2 == 0 && nb / 2 >= 64 && w16_lds<F, 2>(g.M < MT ? g.M : MT, g.K) <= W16_LDS_MAX)
+        return w16_launch<F, MT, 2, 64, 1024>(g, st);
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return w16_launch<F, MT, 4, 32, 512>(g, st);
         return w16_launch<F, MT, 4, 4, 256>(g, st);
