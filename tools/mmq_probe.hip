@@ -87,15 +87,12 @@ int main() {
         VA(16, 2, 8, 3, "abl3 act-only bn16 tt2 w8")
         VA(16, 2, 8, 4, "abl4 wt-only bn16 tt2 w8")
 #undef VA
-#define VS(BN, TT, W, NB, SB, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB, SB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB, ABL, false, SB>(g, st) : hipErrorInvalidValue; }});
-        VS(32, 1, 8, 2, 8, 0, "sb8 bn32 tt1 w8 nb2")
-        VS(32, 1, 8, 2, 8, 1, "sb8 abl1 loads bn32 tt1 w8")
-        VS(32, 1, 4, 2, 8, 0, "sb8 bn32 tt1 w4 nb2")
-        VS(32, 1, 4, 3, 8, 0, "sb8 bn32 tt1 w4 nb3")
-        VS(16, 1, 8, 2, 8, 0, "sb8 bn16 tt1 w8 nb2")
-        VS(32, 2, 4, 2, 8, 0, "sb8 bn32 tt2 w4 nb2")
-#undef VS
+#define VW(BN, TT, W, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB>(g, st) : hipErrorInvalidValue; }});
+        VW(32, 1, 16, 2, "w16 bn32 tt1 nb2")
+        VW(16, 1, 16, 2, "w16 bn16 tt1 nb2")
+        VW(32, 1, 12, 2, "w12 bn32 tt1 nb2")
+#undef VW
 #undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
