@@ -278,6 +278,21 @@ def main() -> None:
         if not torch.equal(bout[0, :, :local], outs[0][0, :, :local]):
             raise RuntimeError("batched GEMV differs from the single-launch GEMV")
 
+    # ---- N > 1: the step's all-gather alone (same bytes, no GEMVs beside it), so the per-GPU kernel
+    #      time and the gather latency are reported separately (SURVEY.md §7, 8-GPU hard part)
+    gather_us = None
+    if world > 1:
+        for _ in range(3):
+            dist.all_gather_into_tensor(gathered[0].view(-1), outs[0].view(-1))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        ng = 20
+        for _ in range(ng):
+            dist.all_gather_into_tensor(gathered[0].view(-1), outs[0].view(-1))
+        torch.cuda.synchronize()
+        gather_us = (time.perf_counter() - g0) / ng * 1e6
+
     # ---- hot (Infinity-Cache resident) reference point: one copy, same launch count
     hot_us = None
     if graphs is not None:
@@ -320,7 +335,8 @@ def main() -> None:
             "data": "synthetic U[-1,1) (torch Generator), quantized on-GPU to Q8_1/Q4_0 by the product's quantizers",
             "config": {"workload": f"{args.wtype}_q8_1_gemv", "M": M, "N": n_total, "K": K,
                        "rows_per_gpu": local, "gemvs_per_step": G, "weight_copies": R,
-                       "parallelism": f"row-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                       "parallelism": f"row-shard x{world}" + (
+                           (" + RCCL all-gather" if backend == "nccl" else f" + {backend} all-gather") if world > 1 else ""),
                        "launch": "hipGraph" if graphs is not None else "eager",
                        "kernel_algo": int(qg.select_algo(M, local, K, wtype)) if args.algo == 0 else args.algo},
             "gbps": round(bytes_per_gemv_all * G * args.steps / elapsed / 1e9, 1),
@@ -337,6 +353,9 @@ def main() -> None:
                 "gbps": round(launch_bytes / batched_us / 1e3, 1),
                 "frac": round(launch_bytes / batched_us / 1e3 / HBM_PEAK_GBPS, 4),
                 "note": f"{G} GEMVs on distinct weight copies per qg_gemm_w4a8_strided_batched launch"},
+            "gather": None if gather_us is None else {
+                "us_per_step": round(gather_us, 2), "bytes_per_rank": G * M * rows * 4,
+                "note": f"all_gather_into_tensor of one step's {G} output slices alone ({backend})"},
             "hot_l3": None if hot_us is None else {"us_per_gemv": round(hot_us, 3),
                                                    "tflops": round(flops_per_gemv / world / hot_us / 1e6, 3)},
         }
