@@ -137,6 +137,19 @@ def test_random_bytes_bit_exact(O, qg, t, algo, m, n, k):
     assert_close_to_oracle(O, c, aq, bq, t)
 
 
+@pytest.mark.parametrize("t", [2, 3, 6, 8])
+@pytest.mark.parametrize("m,n,k", [(1, 70, 14336), (2, 33, 8192), (4, 40, 12288), (3, 17, 6144)])
+def test_gemv_long_rows(O, qg, t, m, n, k):
+    """GEMV shapes whose lanes own several units (the unit loop with preloaded records), incl. a
+    partial last round of units (K = 14336: 224 two-block units over 64 lanes)."""
+    _, _, aq, bq = make_case(O, m, n, k, t)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=ALGOS["gemv"]))
+    assert_close_to_oracle(O, c, aq, bq, t)
+    aq2, bq2 = random_byte_case(m, n, k, t)
+    c2 = host(qg.gemm_w4a8(dev(aq2), dev(bq2), m, n, k, t, algo=ALGOS["gemv"]))
+    assert_close_to_oracle(O, c2, aq2, bq2, t)
+
+
 # ------------------------------------------------------------------------------- outputs
 @pytest.mark.parametrize("t", WTYPES)
 @pytest.mark.parametrize("m", [1, 2, 3, 4, 5, 8])
