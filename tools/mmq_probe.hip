@@ -87,12 +87,6 @@ int main() {
         VA(16, 2, 8, 3, "abl3 act-only bn16 tt2 w8")
         VA(16, 2, 8, 4, "abl4 wt-only bn16 tt2 w8")
 #undef VA
-#define VW(BN, TT, W, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB>(g, st) : hipErrorInvalidValue; }});
-        VW(32, 1, 16, 2, "w16 bn32 tt1 nb2")
-        VW(16, 1, 16, 2, "w16 bn16 tt1 nb2")
-        VW(32, 1, 12, 2, "w12 bn32 tt1 nb2")
-#undef VW
 #undef VN
 #undef V
         auto args = [&](int i) { GemmArgs g; g.A = a; g.B = w[i % R]; g.C = c; g.M = s.M; g.N = s.N; g.K = s.K;
