@@ -76,7 +76,21 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * (include/gemm_cuda_naive.cuh:267-274, gemm_cuda_tiled.cuh:284-291) and gemm_w8a16_naive
  * (gemm_cuda_naive.cuh:276-283); device twin of gemm_w4a16_reference (gemm_reference.h:73-112).
  * Results agree with the reference to fp32 summation order (each block's products are summed,
- * then scaled by d once). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0. */
+ * then scaled by d once). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
+ * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
+ * tiles live in a workspace the library allocates once per (device, stream), on the first such
+ * call outside stream capture (a captured first call runs without split-K, same results to fp32
+ * summation order). qg_release_workspaces() frees them (after a device synchronize).
+ * The _ws forms take the caller's workspace instead (for graphs and multi-stream callers):
+ * >= qg_gemm_w16_workspace_size(M, N, K) bytes (0: no split-K for this shape), 256-B aligned,
+ * zeroed once before its first use — every call leaves it zeroed again; calls that may run
+ * concurrently need distinct workspaces. A smaller or misaligned workspace is not used. */
+void qg_release_workspaces(void);
+size_t qg_gemm_w16_workspace_size(int M, int N, int K);
+int qg_gemm_w4a16_ws(const float* A, const void* B_q4_0, float* C, int M, int N, int K, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream);
+int qg_gemm_w8a16_ws(const float* A, const void* B_q8_0, float* C, int M, int N, int K, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream);
 int qg_gemm_w4a16(const float* A, const void* B_q4_0, float* C, int M, int N, int K, qg_stream_t stream);
 int qg_gemm_w8a16(const float* A, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream);
 /* python/quant_gemm/csrc/gemm_ops.cu:431-466 gemm_q4_0_fp32_cuda(weight_q [N][K/32], activation

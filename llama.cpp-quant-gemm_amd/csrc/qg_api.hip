@@ -1,13 +1,67 @@
 // qg_api.hip — the C-ABI (include/qg/qg.h): validation, dispatch, error reporting.
 //
-// No host synchronisation, no allocation: every entry point only validates, picks a kernel family
-// and enqueues on the caller's stream, so callers may capture it into a hipGraph.
+// No host synchronisation: every entry point validates, picks a kernel family and enqueues on the
+// caller's stream, so callers may capture it into a hipGraph. The one allocation is the split-K
+// workspace of the W4A16 / W8A16 prefill (stream_workspace below): made once per (device, stream)
+// outside capture; a captured first call runs the kernel without split-K instead.
 #include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "../../include/qg/qg.h"
 #include "qg_kernels.hpp"
 
 using namespace qg;
+
+namespace qg {
+namespace {
+std::mutex g_ws_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_ws;
+}  // namespace
+
+void* stream_workspace(hipStream_t st, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto& e = g_ws[{dev, st}];
+    if (e.first && e.second >= bytes) return e.first;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const size_t sz = std::max(bytes, (size_t)4 << 20);
+    void* p = nullptr;
+    if (hipMalloc(&p, sz) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (hipMemsetAsync(p, 0, sz, st) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        return nullptr;
+    }
+    if (e.first) {
+        (void)hipStreamSynchronize(st);  // launches still queued on st may use the old block
+        (void)hipFree(e.first);
+    }
+    e = {p, sz};
+    return p;
+}
+
+void release_workspaces() {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& kv : g_ws)
+        if (kv.second.first) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(kv.second.first);
+        }
+    g_ws.clear();
+}
+}  // namespace qg
 
 namespace {
 thread_local int g_last_hip = 0;
@@ -95,7 +149,8 @@ int weight_major(int wtype, const void* W, const void* A, float* out, int M, int
     g.ldc_m = 1; g.ldc_n = N;
     return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)s);
 }
-int run_w16(int wtype, const float* A, const void* B, float* C, int M, int N, int K, hipStream_t st) {
+int run_w16(int wtype, const float* A, const void* B, float* C, int M, int N, int K, hipStream_t st,
+            void* ws = nullptr, size_t ws_bytes = 0) {
     if (M < 0 || N < 0) return QG_ERR_INVALID_ARG;
     if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
     if (M == 0 || N == 0) return QG_OK;
@@ -104,6 +159,7 @@ int run_w16(int wtype, const float* A, const void* B, float* C, int M, int N, in
     GemmArgs g;
     g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
     g.ldc_m = N; g.ldc_n = 1;
+    g.ws = ws; g.ws_bytes = ws_bytes;
     return hip_status(launch_w16(g, st));
 }
 
@@ -187,6 +243,8 @@ int run_fused(GemmArgs g, void* ws, size_t ws_bytes, hipStream_t st) {
 
 extern "C" {
 
+void qg_release_workspaces(void) { release_workspaces(); }
+
 size_t qg_gemm_w4a8_f32_workspace_size(int M, int K) { return fused_workspace_bytes(M, K); }
 
 int qg_gemm_w4a16(const float* A, const void* B_q4_0, float* C, int M, int N, int K, qg_stream_t stream) {
@@ -195,6 +253,18 @@ int qg_gemm_w4a16(const float* A, const void* B_q4_0, float* C, int M, int N, in
 
 int qg_gemm_w8a16(const float* A, const void* B_q8_0, float* C, int M, int N, int K, qg_stream_t stream) {
     return run_w16(QG_TYPE_Q8_0, A, B_q8_0, C, M, N, K, (hipStream_t)stream);
+}
+
+size_t qg_gemm_w16_workspace_size(int M, int N, int K) { return M > 0 && N > 0 ? w16_workspace_bytes(M, N, K) : 0; }
+
+int qg_gemm_w4a16_ws(const float* A, const void* B_q4_0, float* C, int M, int N, int K, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream) {
+    return run_w16(QG_TYPE_Q4_0, A, B_q4_0, C, M, N, K, (hipStream_t)stream, workspace, workspace_bytes);
+}
+
+int qg_gemm_w8a16_ws(const float* A, const void* B_q8_0, float* C, int M, int N, int K, void* workspace,
+                     size_t workspace_bytes, qg_stream_t stream) {
+    return run_w16(QG_TYPE_Q8_0, A, B_q8_0, C, M, N, K, (hipStream_t)stream, workspace, workspace_bytes);
 }
 
 int qg_gemm_q4_0_fp32(const void* weight_q4_0, const float* activation, float* out, int M, int N, int K,

@@ -21,6 +21,8 @@ struct GemmArgs {
     long ldc_m = 0, ldc_n = 1;
     int batch = 1;               // strided batch of independent products (GEMV path)
     long sA = 0, sB = 0, sC = 0; // batch strides: bytes, bytes, floats
+    void* ws = nullptr;          // optional device workspace (split-K partials + tile counters)
+    size_t ws_bytes = 0;
 };
 
 // GEMV / small batch (M <= 8), register-resident super-block decode + v_dot4.
@@ -35,10 +37,20 @@ hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
 hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
 
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.
+// g.ws / g.ws_bytes: optional caller workspace for the split-K prefill (>= w16_workspace_bytes,
+// 256-B aligned, zero before its first use; left zero by every launch).
 hipError_t launch_w16(const GemmArgs& g, hipStream_t st);
+size_t w16_workspace_bytes(int M, int N, int K);
 
 // FP32 GEMM C = A . B^T (the unquantized baseline), A = float[M][K], B = float[N][K].
 hipError_t launch_fp32(const GemmArgs& g, hipStream_t st);
+
+// Device workspace owned by the library for stream st (split-K partials and tile counters):
+// at least `bytes`, zeroed when first allocated, reused by every later launch on st (launches on
+// one stream are ordered, and every split-K launch leaves its counters zero). nullptr when it
+// cannot be allocated right now (e.g. the stream is being captured): callers fall back to a
+// kernel without a workspace.
+void* stream_workspace(hipStream_t st, size_t bytes);
 
 // Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);

@@ -136,10 +136,16 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // ABL (tuning probes only; the product uses 0): 1 = the DMA stream and waits without any compute,
 // 2 = operand reads + MFMAs without the VALU epilogue, 3 / 4 = as 1 with only the activation /
 // only the weight pieces fetched (the other lanes re-read a line already in flight).
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4>
+// KS > 1: split-K across workgroups — blockIdx.z = slice of H / KS consecutive stages; each slice's
+// fixed-order partial tile goes to the workspace and the last slice to finish (agent-scope counter
+// per output tile) sums the KS partials in slice order (deterministic: the same order whichever
+// workgroup arrives last) and re-arms the counter to 0 for the next launch.
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
+          int KS = 1>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
-                                                     int N, int K, long ldc_m, long ldc_n) {
+                                                     int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
+                                                     unsigned* __restrict__ cnt) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
     using T = wfmt<F>;
     static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
@@ -152,7 +158,8 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * G::NTOK;
     const int nb = K / QK;
-    const int H = nb / SB;  // stages
+    const int H = nb / SB / KS;  // stages of this workgroup's K slice
+    const int h0 = KS > 1 ? (int)blockIdx.z * H : 0;
     const long RB = (long)nb * T::BB;
     const long AB = (long)nb * Q8_1_BYTES;
     uint8_t* bufs = smem + wave * NB * G::BUF;
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     const int rot = ROT && H % W == 0 ? (int)(((blockIdx.x >> 3) * W) % H) : 0;
     auto stage = [&](int k) {
         const int h = wave + rot + k * W;
-        return h >= H ? h - H : h;
+        return h0 + (h >= H ? h - H : h);
     };
 #pragma unroll
     for (int k = 0; k < NB; ++k)
@@ -380,15 +387,47 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 #pragma unroll
         for (int i = 0; i < G::NACC; ++i) red[(wave * G::NACC + i) * 64 + lane] = acc[i];
         __syncthreads();
-        for (int idx = threadIdx.x; idx < G::NACC * 64; idx += W * 64) {
+        constexpr int TS = G::NACC * 64;  // floats per tile
+        auto wsum = [&](int idx) {
             float v = red[idx];
 #pragma unroll
-            for (int ww = 1; ww < W; ++ww) v += red[ww * G::NACC * 64 + idx];
+            for (int ww = 1; ww < W; ++ww) v += red[ww * TS + idx];
+            return v;
+        };
+        auto store = [&](int idx, float v) {
             const int a = idx >> 6, ln = idx & 63;
             const int e = a & 3, t = (a >> 2) % TT, i = (a >> 2) / TT;
             const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
             const int m = m0 + 16 * t + (ln & 15);
             if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
+        };
+        if constexpr (KS == 1) {
+            for (int idx = threadIdx.x; idx < TS; idx += W * 64) store(idx, wsum(idx));
+        } else {
+            const long tile = (long)blockIdx.y * gridDim.x + blockIdx.x;
+            float* pt = part + tile * KS * TS;
+            // Partials and counter move with agent-scope (sc1) accesses, coherent across the XCDs'
+            // L2s without a release/acquire fence: a fence writes back / invalidates a whole L2,
+            // which other workgroups' cached lines pay for (measured 5-40x slower launches).
+            for (int idx = threadIdx.x; idx < TS; idx += W * 64)
+                __hip_atomic_store(pt + blockIdx.z * TS + idx, wsum(idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is at the coherence point
+            __syncthreads();
+            int* last = reinterpret_cast<int*>(smem);
+            if (threadIdx.x == 0)
+                *last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+            __syncthreads();
+            if (!*last) return;
+            for (int idx = threadIdx.x; idx < TS; idx += W * 64) {
+                float x[KS];  // every slice's load issued before the first add (atomic loads keep order)
+#pragma unroll
+                for (int s = 0; s < KS; ++s) x[s] = __hip_atomic_load(pt + s * TS + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                float v = x[0];
+#pragma unroll
+                for (int s = 1; s < KS; ++s) v += x[s];
+                store(idx, v);
+            }
+            if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #ifdef QG_MMQ_STAMPS
@@ -403,10 +442,20 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
 // rows and stages aligned to the DMA piece, 32-bit byte offsets. P16 additionally: a 16-B aligned B
 // and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_geom).
-template <int F, int BN, int TT, int W, bool P16, int NB = 2, int SB = 4>
+// Workspace of a split-K (KS > 1) launch: one counter per output tile (zero before the first
+// launch; every launch leaves them zero), then KS partial tiles per output tile.
+template <int BN, int TT, int KS> inline size_t mmq_ws_bytes(int M, int N) {
+    if (KS == 1) return 0;
+    const size_t tiles = (size_t)((N + BN - 1) / BN) * ((M + 16 * TT - 1) / (16 * TT));
+    return ((tiles * 4 + 255) & ~(size_t)255) + tiles * KS * (BN / 16) * TT * 4 * 64 * 4;
+}
+
+template <int F, int BN, int TT, int W, bool P16, int NB = 2, int SB = 4, int KS = 1>
 inline bool mmq_shape_ok(const GemmArgs& g) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
-    if (g.M < 1 || g.N < 1 || g.K % (QK * SB) != 0) return false;
+    if (g.M < 1 || g.N < 1 || g.K % (QK * SB * KS) != 0) return false;
+    if (KS > 1 && (g.sumi || !g.ws || g.ws_bytes < mmq_ws_bytes<BN, TT, KS>(g.M, g.N) || ((uintptr_t)g.ws & 255)))
+        return false;
     const long RB = (long)(g.K / QK) * wfmt<F>::BB, AB = (long)(g.K / QK) * Q8_1_BYTES;
     if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
     if (P16 && G::RSB % 16 != 0 && g.K % 256 != 0) return false;
@@ -415,11 +464,14 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     return true;
 }
 
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4>
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
+          int KS = 1>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
-    const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB>;
+    const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK, KS);
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS>;
+    unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;
+    float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
     if (G::LDS > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {
@@ -429,7 +481,7 @@ hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
         }
     }
     hipLaunchKernelGGL(k, grid, dim3(W * 64), G::LDS, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.C, g.sumi, g.M,
-                       g.N, g.K, g.ldc_m, g.ldc_n);
+                       g.N, g.K, g.ldc_m, g.ldc_n, part, cnt);
     return hipGetLastError();
 }
 

@@ -187,6 +187,7 @@ __global__ __launch_bounds__(256) void w16_generic_kernel(const float* __restric
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t hi16_pack(uint32_t lo_elem, uint32_t hi_elem) {
     return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // {lo_elem[31:16], hi_elem[31:16]}
@@ -334,6 +335,204 @@ __global__ __launch_bounds__(W * 64) void w16_mfma_kernel(const float* __restric
     }
 }
 
+// Split-K prefill (M > 8; round-1 second design, replaces w16_mfma_kernel where it applies).
+// w16_mfma_kernel re-reads and re-splits all M x K fp32 activations in every workgroup (512 KB per
+// workgroup at M = 32, K = 4096: 26 us). Here a workgroup owns 16 RT weight rows x 16 TT tokens x
+// one K slice (blockIdx.z): it splits each activation once into hi / mid / lo bf16 fragment images
+// in LDS (lane-linear, one ds_read_b128 per operand), every wave owns one 16-row tile and takes its
+// weights straight from HBM into registers (all KB blocks of a chunk in flight before the staging
+// starts). Operands are swapped against w16_mfma_kernel — A = tokens, B = weight rows — so a
+// lane's output column is its own weight row and the block scale d_w is a per-lane scalar. The
+// KS slices' partial tiles meet through the workspace as in mmq_kernel (KS > 1): agent-scope
+// stores, a per-tile counter, the last slice sums the partials in slice order and re-arms it.
+// Weight k-slot q of a block: elements 8q..8q+7 = nibble plane q>>1 of qs[8(q&1)..] (Q4_0) or
+// qs[8q..] (Q8_0); the activation fragments use the same element order.
+template <int F> __device__ __forceinline__ u32x4_t w16_wfrag(uint32_t x, uint32_t y, int sh) {
+    // bytes of x, y (nibbles at shift sh for Q4_0, sign-flipped bytes for Q8_0) -> exact bf16 of
+    // q - 8 (Q4_0) or q (Q8_0): unsigned byte -> f32 (v_cvt_f32_ubyte*), minus the offset
+    uint32_t u0, u1;
+    float off;
+    if constexpr (F == FMT_Q8_0) { u0 = x ^ 0x80808080u; u1 = y ^ 0x80808080u; off = -128.0f; }
+    else { u0 = (x >> sh) & 0x0F0F0F0Fu; u1 = (y >> sh) & 0x0F0F0F0Fu; off = -8.0f; }
+    const f32x2 o = {off, off};
+    f32x2 v[4];
+    v[0] = f32x2{(float)(u0 & 0xFFu), (float)((u0 >> 8) & 0xFFu)} + o;
+    v[1] = f32x2{(float)((u0 >> 16) & 0xFFu), (float)(u0 >> 24)} + o;
+    v[2] = f32x2{(float)(u1 & 0xFFu), (float)((u1 >> 8) & 0xFFu)} + o;
+    v[3] = f32x2{(float)((u1 >> 16) & 0xFFu), (float)(u1 >> 24)} + o;
+    u32x4_t r;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) r[p] = hi16_pack(__float_as_uint(v[p].x), __float_as_uint(v[p].y));
+    return r;
+}
+
+template <int F, int RT, int TT, int KB>
+__global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
+                                                         float* __restrict__ C, int M, int N, int K, long ldc_m,
+                                                         long ldc_n, int kbs, float* __restrict__ part,
+                                                         unsigned* __restrict__ cnt) {
+    using T = wfmt<F>;
+    static_assert(F == FMT_Q4_0 || F == FMT_Q8_0, "Q4_0 / Q8_0 weights");
+    static_assert(KB % 4 == 0 && (TT * KB) % RT == 0, "whole block groups, whole staging rounds");
+    constexpr int FR = 1024;             // bytes per fragment image: 64 lanes x 16 B
+    constexpr int SJ = TT * KB / RT;     // staging items per thread per chunk
+    constexpr int GB = TT >= 4 ? 2 : 4;  // blocks per compute group (operand registers)
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ int s_last;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, r16 = lane & 15, q = lane >> 4;
+    const int n0 = blockIdx.x * 16 * RT, m0 = blockIdx.y * 16 * TT;
+    const int nb = K / QK;
+    const long RB = (long)nb * T::BB;
+    const int n = n0 + 16 * wave + r16;  // this lane's weight row (its output column)
+    const uint8_t* wrow = B + (long)min(n, N - 1) * RB;
+    const int qoff = T::QS + (T::Q8 ? 8 * q : 8 * (q & 1));  // its 8 bytes in a block (even: +2 mod 4)
+    const int sh = T::Q8 ? 0 : 4 * (q >> 1);
+
+    f32x4_t acc[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int c0 = 0; c0 < kbs; c0 += KB) {
+        const int kb0 = blockIdx.z * kbs + c0;  // even (KB even, kbs a multiple of KB)
+        // 1) the chunk's weight bytes in flight: rows are 4-B aligned (nb even), a block's 8 bytes
+        //    start 2 bytes into a dword in even blocks (3 dwords) and on a dword in odd ones
+        uint32_t wx[KB], wy[KB], wz[KB], wd[KB];
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const uint8_t* blk = wrow + (long)(kb0 + b) * T::BB;
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(blk + ((qoff + (b & 1) * 2) & ~3) - (b & 1) * 2);
+            wx[b] = p[0];
+            wy[b] = p[1];
+            wz[b] = (b & 1) ? 0u : p[2];
+            wd[b] = *reinterpret_cast<const uint16_t*>(blk);
+        }
+        // 2) activation fragments: token 16 t + (lane & 15), elements 8 (lane >> 4) .. + 8 of block b
+        float4 x[SJ][2];
+#pragma unroll
+        for (int j = 0; j < SJ; ++j) {
+            const int it = threadIdx.x + j * RT * 64, ln = it & 63, tb = it >> 6;
+            const int t = tb % TT, b = tb / TT;
+            const int m = min(m0 + 16 * t + (ln & 15), M - 1);
+            const float4* p = reinterpret_cast<const float4*>(A + (long)m * K + (long)(kb0 + b) * QK + 8 * (ln >> 4));
+            x[j][0] = p[0];
+            x[j][1] = p[1];
+        }
+#pragma unroll
+        for (int j = 0; j < SJ; ++j) {
+            const int it = threadIdx.x + j * RT * 64;
+            u32x4_t h, mi, lo;
+            w16_afrag(x[j][0], x[j][1], h, mi, lo);
+            u32x4_t* dst = reinterpret_cast<u32x4_t*>(lds + (size_t)(it >> 6) * 3 * FR) + (it & 63);
+            dst[0] = h;
+            dst[64] = mi;
+            dst[128] = lo;
+        }
+        __syncthreads();
+        // 3) GB blocks at a time: operand reads + weight decode, 3 GB TT MFMAs, then the d_w epilogue
+        //    (MFMA results read behind an explicit wait, as in mmq_kernel)
+#pragma unroll
+        for (int g = 0; g < KB; g += GB) {
+            u32x4_t wf[GB], af[GB][TT][3];
+            float dw[GB];
+            f32x4_t c[GB][TT];
+#pragma unroll
+            for (int bb = 0; bb < GB; ++bb) {
+                const int b = g + bb;
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const u32x4_t* fa = reinterpret_cast<const u32x4_t*>(lds + (size_t)(b * TT + t) * 3 * FR) + lane;
+                    af[bb][t][0] = fa[0];
+                    af[bb][t][1] = fa[64];
+                    af[bb][t][2] = fa[128];
+                }
+                const uint32_t xl = (b & 1) ? wx[b] : __builtin_amdgcn_alignbyte(wy[b], wx[b], 2);
+                const uint32_t yl = (b & 1) ? wy[b] : __builtin_amdgcn_alignbyte(wz[b], wy[b], 2);
+                wf[bb] = w16_wfrag<F>(xl, yl, sh);
+                dw[bb] = h2f(wd[b]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int bb = 0; bb < GB; ++bb)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const bf16x8_t wb = __builtin_bit_cast(bf16x8_t, wf[bb]);
+                    f32x4_t r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][0]), wb,
+                                                                        f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][1]), wb, r, 0, 0, 0);
+                    c[bb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][2]), wb, r, 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int bb = 0; bb < GB; ++bb)
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[t][e] = __builtin_fmaf(dw[bb], c[bb][t][e], acc[t][e]);
+        }
+        __syncthreads();  // every wave done with the fragments before the next chunk's staging
+    }
+
+    // lane: column n, rows (tokens) m0 + 16 t + 4 q + e
+    auto store = [&](int t, int e, float v) {
+        const int m = m0 + 16 * t + 4 * q + e;
+        if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
+    };
+    if (gridDim.z == 1) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) store(t, e, acc[t][e]);
+        return;
+    }
+    constexpr int TS = RT * TT * 4 * 64;  // floats per partial tile
+    const int KS = gridDim.z;
+    const long tile = (long)blockIdx.y * gridDim.x + blockIdx.x;
+    float* pt = part + tile * KS * TS;
+    auto pidx = [&](int t, int e) { return ((wave * TT + t) * 4 + e) * 64 + lane; };
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            __hip_atomic_store(pt + blockIdx.z * TS + pidx(t, e), acc[t][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)KS - 1;
+    __syncthreads();
+    if (!s_last) return;
+    // slice-order sum; each round's loads are all issued before its first add (atomic loads keep
+    // program order, so a load-add chain would wait out one memory latency per slice)
+    float v[TT][4];
+    for (int s0 = 0; s0 < KS; s0 += 4) {
+        float x[4][TT][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    x[j][t][e] = __hip_atomic_load(pt + min(s0 + j, KS - 1) * TS + pidx(t, e), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (s0 + j == 0) v[t][e] = x[j][t][e];
+                    else if (s0 + j < KS) v[t][e] += x[j][t][e];
+                }
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) store(t, e, v[t][e]);
+    if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 namespace {
 constexpr int W16_MT = 8;
 constexpr size_t W16_LDS_MAX = 160 * 1024;
@@ -391,7 +590,73 @@ template <int F, int RT, int TT, int W> hipError_t w16_mfma_launch(const GemmArg
     return hipGetLastError();
 }
 
+// Split-K prefill plan: RT 16-row tiles (one per wave) x 16 TT tokens x ks slices of K, KB blocks
+// per LDS chunk. ks: the fewest slices (a divisor of the chunk count) that give >= 256 workgroups.
+struct w16_plan {
+    int rt = 0, tt = 0, kb = 0, ks = 1;
+    long gx = 0, gy = 0;
+    size_t ws_bytes = 0;  // workspace for ks > 1: tile counters, then ks partial tiles per tile
+};
+
+w16_plan w16_make_plan(int M, int N, int K) {
+    w16_plan p;
+    const int nb = K / QK;
+    if (M <= 8 || K % QK != 0) return p;
+    if (M <= 64 && nb % 16 == 0) { p.tt = 2; p.kb = 16; }
+    else if (M > 64 && nb % 8 == 0) { p.tt = 4; p.kb = 8; }
+    else return p;
+    p.rt = N >= 2048 ? 8 : 4;
+    p.gx = (N + 16 * p.rt - 1) / (16 * p.rt);
+    p.gy = (M + 16 * p.tt - 1) / (16 * p.tt);
+    const int chunks = nb / p.kb;
+    if (p.gx * p.gy < 256)
+        for (int d = 2; d <= chunks && d <= 32; ++d) {
+            if (chunks % d) continue;
+            p.ks = d;
+            if (p.gx * p.gy * d >= 256) break;
+        }
+    if (p.ks > 1)
+        p.ws_bytes = ((size_t)p.gx * p.gy * 4 + 255) / 256 * 256 + (size_t)p.gx * p.gy * p.ks * p.rt * p.tt * 4 * 64 * 4;
+    return p;
+}
+
+template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs& g, const w16_plan& p, void* ws,
+                                                                  hipStream_t st) {
+    const int ks = ws ? p.ks : 1;
+    unsigned* cnt = (unsigned*)ws;
+    float* part = ws ? (float*)((uint8_t*)ws + ((size_t)p.gx * p.gy * 4 + 255) / 256 * 256) : nullptr;
+    constexpr size_t lds = (size_t)TT * KB * 3 * 1024;
+    auto kfn = w16_sk_kernel<F, RT, TT, KB>;
+    if (lds > 64 * 1024) {
+        static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
+        if (!attr_set) {
+            hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+    }
+    hipLaunchKernelGGL(kfn, dim3(p.gx, p.gy, ks), dim3(RT * 64), lds, st, (const float*)g.A, (const uint8_t*)g.B, g.C,
+                       g.M, g.N, g.K, g.ldc_m, g.ldc_n, g.K / QK / ks, part, cnt);
+    return hipGetLastError();
+}
+
 template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
+    if (((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 3) == 0 && (g.M + 63) / 64 <= 65535) {
+        const w16_plan p = w16_make_plan(g.M, g.N, g.K);
+        if (p.rt) {
+            // the caller's workspace (qg_gemm_w4a16_ws), else the library's one for this stream
+            void* ws = nullptr;
+            if (p.ks > 1) {
+                if (g.ws) ws = g.ws_bytes >= p.ws_bytes && ((uintptr_t)g.ws & 255) == 0 ? g.ws : nullptr;
+                else ws = stream_workspace(st, p.ws_bytes);
+            }
+            // without one, a grid this small would leave most CUs idle: the older kernel below
+            if (ws || p.ks == 1 || p.gx * p.gy >= 128) {
+                if (p.tt == 2) return p.rt == 8 ? w16_sk_launch<F, 8, 2, 16>(g, p, ws, st) : w16_sk_launch<F, 4, 2, 16>(g, p, ws, st);
+                return p.rt == 8 ? w16_sk_launch<F, 8, 4, 8>(g, p, ws, st) : w16_sk_launch<F, 4, 4, 8>(g, p, ws, st);
+            }
+        }
+    }
     if (g.M > 8 && ((uintptr_t)g.A & 15) == 0 && (g.M + 31) / 32 <= 65535) {
         // one 16-row tile per workgroup while that leaves < 256 workgroups of 32 rows
         if ((long)((g.N + 31) / 32) * ((g.M + 31) / 32) < 256) return w16_mfma_launch<F, 1, 2, 16>(g, st);
@@ -409,6 +674,8 @@ template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
     return hipGetLastError();
 }
 }  // namespace
+
+size_t w16_workspace_bytes(int M, int N, int K) { return w16_make_plan(M, N, K).ws_bytes; }
 
 hipError_t launch_w16(const GemmArgs& g, hipStream_t st) {
     switch (g.wtype) {

@@ -40,6 +40,10 @@ SIGNATURES = {
     "qg_gemm_w4a16": ([P, P, P, I, I, I, P], I),
     "qg_gemm_w8a16": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_0_fp32": ([P, P, P, I, I, I, P], I),
+    "qg_gemm_w16_workspace_size": ([I, I, I], SZ),
+    "qg_gemm_w4a16_ws": ([P, P, P, I, I, I, P, SZ, P], I),
+    "qg_gemm_w8a16_ws": ([P, P, P, I, I, I, P, SZ, P], I),
+    "qg_release_workspaces": ([], None),
     "qg_quantize_q8_1": ([P, P, I64, P], I),
     "qg_quantize_q4_0": ([P, P, I64, P], I),
     "qg_quantize": ([I, I, P, P, I64, P], I),

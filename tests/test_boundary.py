@@ -68,6 +68,11 @@ def test_static_queries(lib):
     assert so.qg_select_algo(16, 64, 4128, 7) == 3
     assert so.qg_select_algo(1, 4096, 33, 2) == -1
     assert so.qg_status_string(-2).decode().startswith("K must be")
+    # W4A16 prefill split-K workspace (host-side plan): 256 workgroups of 128 rows x 32 tokens x
+    # K/8 at M=32, N=K=4096 -> 32 tiles x 8 slices x 16 KB of partials + the tile counters
+    assert so.qg_gemm_w16_workspace_size(32, 4096, 4096) == 256 + 32 * 8 * 8 * 2 * 4 * 64 * 4
+    assert so.qg_gemm_w16_workspace_size(4, 4096, 4096) == 0      # GEMV: no workspace
+    assert so.qg_gemm_w16_workspace_size(512, 4096, 4096) == 0    # enough token tiles: no split
 
 
 def test_validation_codes_without_launch(lib):

@@ -70,3 +70,65 @@ def test_w4a16_unaligned_activation_generic_path(O, qg):
     P = ctypes.c_void_p
     assert lib.qg_gemm_w4a16(P(x.data_ptr()), P(dev(bq).data_ptr()), P(c.data_ptr()), m, n, k, st) == 0
     check(O, host(c), a, bq, 2)
+
+
+# Prefill (M > 8, K % 256 == 0): the split-K kernel (w16_sk_kernel) — K slices across workgroups
+# meet through the library's per-stream workspace; 16-token tiles (M <= 64) and 64-token tiles,
+# 64- and 128-row workgroups, ragged M and N, several slices per chunk count.
+@pytest.mark.parametrize("t", [2, 8])
+@pytest.mark.parametrize("m,n,k", [(32, 4096, 4096), (17, 300, 1024), (64, 2048, 2048), (100, 256, 2048),
+                                   (130, 2100, 512), (40, 640, 14336), (9, 33, 512), (65, 16, 256)])
+def test_w16_prefill_split_k(O, qg, t, m, n, k):
+    a, b = O.fill_uniform_step4(m, n, k, seed=m * 7 + n)
+    bq = O.quantize(b, t)
+    fn = qg.gemm_w4a16 if t == 2 else qg.gemm_w8a16
+    ad, bd = dev(a), dev(bq)
+    c1 = host(fn(ad, bd, m, n, k))
+    check(O, c1, a, bq, t)
+    # the tile counters re-arm themselves: a second launch is bit-identical
+    c2 = host(fn(ad, bd, m, n, k))
+    assert np.array_equal(c1, c2)
+
+
+def test_w16_prefill_split_k_second_stream(O, qg):
+    """Each stream gets its own workspace; results are bit-identical across streams."""
+    import torch
+    m, n, k = 32, 1024, 4096
+    a, b = O.fill_uniform_step4(m, n, k, seed=5)
+    bq = O.quantize(b, 2)
+    ad, bd = dev(a), dev(bq)
+    c0 = host(qg.gemm_w4a16(ad, bd, m, n, k))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        c1 = qg.gemm_w4a16(ad, bd, m, n, k)
+    s.synchronize()
+    assert np.array_equal(c0, host(c1))
+    check(O, c0, a, bq, 2)
+
+
+@pytest.mark.parametrize("t", [2, 8])
+def test_w16_prefill_caller_workspace(O, qg, t):
+    """qg_gemm_w{4,8}a16_ws: the caller's zeroed workspace, left zeroed; too small -> not used."""
+    import torch
+    m, n, k = 24, 2048, 2048
+    a, b = O.fill_uniform_step4(m, n, k, seed=t)
+    bq = O.quantize(b, t)
+    lib = qg._lib.load()
+    need = lib.qg_gemm_w16_workspace_size(m, n, k)
+    assert need > 0
+    ws = torch.zeros(need // 4 + 64, dtype=torch.int32, device="cuda")
+    P = ctypes.c_void_p
+    st = P(torch.cuda.current_stream().cuda_stream)
+    sym = lib.qg_gemm_w4a16_ws if t == 2 else lib.qg_gemm_w8a16_ws
+    ad, bd = dev(a), dev(bq)
+    outs = []
+    for nbytes in (need, need, 64):
+        c = torch.empty((m, n), dtype=torch.float32, device="cuda")
+        assert sym(P(ad.data_ptr()), P(bd.data_ptr()), P(c.data_ptr()), m, n, k, P(ws.data_ptr()), nbytes, st) == 0
+        torch.cuda.synchronize()
+        outs.append(host(c))
+        # counters re-armed: every tile counter is zero again after the launch
+        assert int(ws[: (need // 4)][:16].abs().sum()) == 0
+    check(O, outs[0], a, bq, t)
+    assert np.array_equal(outs[0], outs[1])
+    check(O, outs[2], a, bq, t)

@@ -77,17 +77,21 @@ def measure_w16(wname: str, M: int, N: int, K: int, G: int, reps: int) -> dict:
     copies.copy_(bq.unsqueeze(0).expand_as(copies))
     out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
     lib = qg._lib.load()
-    sym = lib.qg_gemm_w4a16 if wt == 2 else lib.qg_gemm_w8a16
+    sym = lib.qg_gemm_w4a16_ws if wt == 2 else lib.qg_gemm_w8a16_ws
+    # the caller-workspace form: a graph captures its own stream, which has no library workspace
+    need = lib.qg_gemm_w16_workspace_size(M, N, K)
+    ws = torch.zeros(max(need, 256) // 4 + 64, dtype=torch.int32, device=dev)
 
     def step(stream):
         for j in range(G):
             assert sym(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
-                       ctypes.c_void_p(out[j].data_ptr()), M, N, K, stream) == 0
+                       ctypes.c_void_p(out[j].data_ptr()), M, N, K, ctypes.c_void_p(ws.data_ptr()), need,
+                       stream) == 0
 
     us = graph_us(step, reps) / G
     byts = wbytes + M * K * 4 + M * N * 4
     flops = 2.0 * M * N * K
-    return {"wtype": wname, "M": M, "N": N, "K": K, "algo": "w16 gemv", "us_per_launch": round(us, 3),
+    return {"wtype": wname, "M": M, "N": N, "K": K, "algo": "w16 gemv" if M <= 8 else f"w16 mfma split-K ws={need}", "us_per_launch": round(us, 3),
             "gbps": round(byts / us / 1e3, 1), "frac_hbm": round(byts / us / 1e3 / PEAK, 4),
             "tflops": round(flops / us / 1e6, 3), "nmse_vs_fp32": nmse, "algorithmic_bytes": byts, "launches": G}
 
