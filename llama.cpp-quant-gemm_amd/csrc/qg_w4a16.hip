@@ -187,6 +187,7 @@ __global__ __launch_bounds__(256) void w16_generic_kernel(const float* __restric
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4a4_t __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t hi16_pack(uint32_t lo_elem, uint32_t hi_elem) {
@@ -366,7 +367,9 @@ template <int F> __device__ __forceinline__ u32x4_t w16_wfrag(uint32_t x, uint32
     return r;
 }
 
-template <int F, int RT, int TT, int KB>
+// ABL (tuning probe only; the product uses 0): 1 = each slice stores its partial tile and exits
+// (no counter, no reduction: timing of the slice work alone).
+template <int F, int RT, int TT, int KB, int ABL = 0>
 __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                          float* __restrict__ C, int M, int N, int K, long ldc_m,
                                                          long ldc_n, int kbs, float* __restrict__ part,
@@ -397,15 +400,31 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
         const int kb0 = blockIdx.z * kbs + c0;  // even (KB even, kbs a multiple of KB)
         // 1) the chunk's weight bytes in flight: rows are 4-B aligned (nb even), a block's 8 bytes
         //    start 2 bytes into a dword in even blocks (3 dwords) and on a dword in odd ones
+        //    Q4_0: a block pair is 36 contiguous bytes (9 dwords, 4-B aligned) — 3 loads per pair
+        //    (x4, x4, x1) instead of 4 per block; the lane's 8 bytes and d of each block are picked
+        //    from them at compute time (PW). Q8_0: 4 loads per block.
+        constexpr bool PW = F == FMT_Q4_0;
         uint32_t wx[KB], wy[KB], wz[KB], wd[KB];
+        u32x4_t pa[PW ? KB / 2 : 1], pb[PW ? KB / 2 : 1];
+        uint32_t pc[PW ? KB / 2 : 1];
+        if constexpr (PW) {
 #pragma unroll
-        for (int b = 0; b < KB; ++b) {
-            const uint8_t* blk = wrow + (long)(kb0 + b) * T::BB;
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(blk + ((qoff + (b & 1) * 2) & ~3) - (b & 1) * 2);
-            wx[b] = p[0];
-            wy[b] = p[1];
-            wz[b] = (b & 1) ? 0u : p[2];
-            wd[b] = *reinterpret_cast<const uint16_t*>(blk);
+            for (int pr = 0; pr < KB / 2; ++pr) {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(wrow + (long)(kb0 + 2 * pr) * T::BB);
+                pa[pr] = *reinterpret_cast<const u32x4a4_t*>(p);
+                pb[pr] = *reinterpret_cast<const u32x4a4_t*>(p + 4);
+                pc[pr] = p[8];
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < KB; ++b) {
+                const uint8_t* blk = wrow + (long)(kb0 + b) * T::BB;
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(blk + ((qoff + (b & 1) * 2) & ~3) - (b & 1) * 2);
+                wx[b] = p[0];
+                wy[b] = p[1];
+                wz[b] = (b & 1) ? 0u : p[2];
+                wd[b] = *reinterpret_cast<const uint16_t*>(blk);
+            }
         }
         // 2) activation fragments: token 16 t + (lane & 15), elements 8 (lane >> 4) .. + 8 of block b
         float4 x[SJ][2];
@@ -446,10 +465,29 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
                     af[bb][t][1] = fa[64];
                     af[bb][t][2] = fa[128];
                 }
-                const uint32_t xl = (b & 1) ? wx[b] : __builtin_amdgcn_alignbyte(wy[b], wx[b], 2);
-                const uint32_t yl = (b & 1) ? wy[b] : __builtin_amdgcn_alignbyte(wz[b], wy[b], 2);
+                uint32_t xl, yl, wdb;
+                if constexpr (PW) {
+                    // pair dwords d0..d8; even block: d = d0.lo, bytes 2+8 q1 .. ; odd: d = d4.hi,
+                    // bytes 20+8 q1 .. (q1 = q & 1)
+                    const u32x4_t& A4 = pa[b >> 1];
+                    const u32x4_t& B4 = pb[b >> 1];
+                    const bool q1 = q & 1;
+                    if ((b & 1) == 0) {
+                        xl = q1 ? __builtin_amdgcn_alignbyte(A4[3], A4[2], 2) : __builtin_amdgcn_alignbyte(A4[1], A4[0], 2);
+                        yl = q1 ? __builtin_amdgcn_alignbyte(B4[0], A4[3], 2) : __builtin_amdgcn_alignbyte(A4[2], A4[1], 2);
+                        wdb = A4[0] & 0xFFFFu;
+                    } else {
+                        xl = q1 ? B4[3] : B4[1];
+                        yl = q1 ? pc[b >> 1] : B4[2];
+                        wdb = B4[0] >> 16;
+                    }
+                } else {
+                    xl = (b & 1) ? wx[b] : __builtin_amdgcn_alignbyte(wy[b], wx[b], 2);
+                    yl = (b & 1) ? wy[b] : __builtin_amdgcn_alignbyte(wz[b], wy[b], 2);
+                    wdb = wd[b];
+                }
                 wf[bb] = w16_wfrag<F>(xl, yl, sh);
-                dw[bb] = h2f(wd[b]);
+                dw[bb] = h2f(wdb);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -497,6 +535,7 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
 #pragma unroll
         for (int e = 0; e < 4; ++e)
             __hip_atomic_store(pt + blockIdx.z * TS + pidx(t, e), acc[t][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (ABL == 1) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
@@ -602,18 +641,22 @@ w16_plan w16_make_plan(int M, int N, int K) {
     w16_plan p;
     const int nb = K / QK;
     if (M <= 8 || K % QK != 0) return p;
-    if (M <= 64 && nb % 16 == 0) { p.tt = 2; p.kb = 16; }
-    else if (M > 64 && nb % 8 == 0) { p.tt = 4; p.kb = 8; }
+    // M <= 64: 64-row x 32-token tiles, 8-block chunks, K split until >= 512 workgroups (two per CU:
+    // one's loads overlap the other's compute); tools/w16_sk_probe.hip, profiles/r01_tuning/
+    // w16_sk_probe.txt: M=32 N=K=4096 16.7 us vs 18.8 for 128-row tiles, 16-block chunks, 256 WGs.
+    // M > 64: 128-row (N >= 2048) or 64-row tiles x 64 tokens, >= 256 workgroups.
+    int want = 256;
+    if (M <= 64 && nb % 8 == 0) { p.tt = 2; p.kb = 8; p.rt = 4; want = 512; }
+    else if (M > 64 && nb % 8 == 0) { p.tt = 4; p.kb = 8; p.rt = N >= 2048 ? 8 : 4; }
     else return p;
-    p.rt = N >= 2048 ? 8 : 4;
     p.gx = (N + 16 * p.rt - 1) / (16 * p.rt);
     p.gy = (M + 16 * p.tt - 1) / (16 * p.tt);
     const int chunks = nb / p.kb;
-    if (p.gx * p.gy < 256)
+    if (p.gx * p.gy < want)
         for (int d = 2; d <= chunks && d <= 32; ++d) {
             if (chunks % d) continue;
             p.ks = d;
-            if (p.gx * p.gy * d >= 256) break;
+            if (p.gx * p.gy * d >= want) break;
         }
     if (p.ks > 1)
         p.ws_bytes = ((size_t)p.gx * p.gy * 4 + 255) / 256 * 256 + (size_t)p.gx * p.gy * p.ks * p.rt * p.tt * 4 * 64 * 4;
@@ -652,7 +695,7 @@ template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
             }
             // without one, a grid this small would leave most CUs idle: the older kernel below
             if (ws || p.ks == 1 || p.gx * p.gy >= 128) {
-                if (p.tt == 2) return p.rt == 8 ? w16_sk_launch<F, 8, 2, 16>(g, p, ws, st) : w16_sk_launch<F, 4, 2, 16>(g, p, ws, st);
+                if (p.tt == 2) return w16_sk_launch<F, 4, 2, 8>(g, p, ws, st);
                 return p.rt == 8 ? w16_sk_launch<F, 8, 4, 8>(g, p, ws, st) : w16_sk_launch<F, 4, 4, 8>(g, p, ws, st);
             }
         }

@@ -48,9 +48,12 @@ def test_library_exports_every_declared_symbol(lib):
     assert set(lib.SIGNATURES) == set(fns), "Python bindings out of sync with qg.h"
 
 
-def test_library_is_gfx950_code_object(lib):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib.LIB_PATH],
-                         capture_output=True, text=True)
+def test_library_is_gfx950_code_object(lib, tmp_path):
+    # llvm-objdump --offloading extracts every bundle next to its input: run it on a copy
+    import shutil
+    so = shutil.copy(lib.LIB_PATH, tmp_path / "libqg_hip.so")
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(so)],
+                         capture_output=True, text=True, cwd=tmp_path)
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out.stdout
@@ -68,9 +71,9 @@ def test_static_queries(lib):
     assert so.qg_select_algo(16, 64, 4128, 7) == 3
     assert so.qg_select_algo(1, 4096, 33, 2) == -1
     assert so.qg_status_string(-2).decode().startswith("K must be")
-    # W4A16 prefill split-K workspace (host-side plan): 256 workgroups of 128 rows x 32 tokens x
-    # K/8 at M=32, N=K=4096 -> 32 tiles x 8 slices x 16 KB of partials + the tile counters
-    assert so.qg_gemm_w16_workspace_size(32, 4096, 4096) == 256 + 32 * 8 * 8 * 2 * 4 * 64 * 4
+    # W4A16 prefill split-K workspace (host-side plan): 512 workgroups of 64 rows x 32 tokens x
+    # K/8 at M=32, N=K=4096 -> 64 tiles x 8 slices x 8 KB of partials + the tile counters
+    assert so.qg_gemm_w16_workspace_size(32, 4096, 4096) == 256 + 64 * 8 * 4 * 2 * 4 * 64 * 4
     assert so.qg_gemm_w16_workspace_size(4, 4096, 4096) == 0      # GEMV: no workspace
     assert so.qg_gemm_w16_workspace_size(512, 4096, 4096) == 0    # enough token tiles: no split
 
