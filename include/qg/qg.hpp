@@ -89,6 +89,12 @@ inline int gemm_w4a16_tiled(const float* A, const qg_block_q4_0* B, float* C, in
                             qg_stream_t stream = nullptr) {
     return qg_gemm_w4a16(A, B, C, M, N, K, stream);
 }
+// W4A16 / W8A16 with a caller-owned split-K workspace (no library allocation; capture-safe)
+inline size_t gemm_w16_workspace_size(int M, int N, int K) { return qg_gemm_w16_workspace_size(M, N, K); }
+inline int gemm_w4a16_ws(const float* A, const qg_block_q4_0* B, float* C, int M, int N, int K, void* ws,
+                         size_t ws_bytes, qg_stream_t stream = nullptr) {
+    return qg_gemm_w4a16_ws(A, B, C, M, N, K, ws, ws_bytes, stream);
+}
 inline int gemm_w8a16_naive(const float* A, const qg_block_q8_0* B, float* C, int M, int N, int K,
                             qg_stream_t stream = nullptr) {
     return qg_gemm_w8a16(A, B, C, M, N, K, stream);
