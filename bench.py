@@ -70,34 +70,63 @@ def load_traffic(cfg_key: str):
     return None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
+    """the reference is single-threaded -> the headline baseline is 1 core, pinned
+    (sched_setaffinity, as taskset), after 1 warm-up, median of the runs; plus a row-partitioned
+    multi-thread run. Bounded to ~`seconds` of CPU work."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O  # the checker / CPU baseline only
     a, b = O.fill_uniform_step4(m, n, k, 42)
     aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, wtype)
-    O.gemm_w4a8(aq, bq, wtype)  # warm-up
-    runs, t0 = 0, time.perf_counter()
-    while True:
-        O.gemm_w4a8(aq, bq, wtype)
-        runs += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    per = el / runs
-    threads = min(16, os.cpu_count() or 1)
+    saved = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    core = min(saved) if saved else None
+    if core is not None:
+        os.sched_setaffinity(0, {core})
+    try:
+        O.gemm_w4a8(aq, bq, wtype)  # warm-up
+        times, t0 = [], time.perf_counter()
+        while True:
+            r0 = time.perf_counter()
+            O.gemm_w4a8(aq, bq, wtype)
+            times.append(time.perf_counter() - r0)
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        if saved is not None:
+            os.sched_setaffinity(0, saved)
+    times.sort()
+    runs = len(times)
+    per = times[runs // 2]
+    threads = min(16, len(saved) if saved else (os.cpu_count() or 1))
     t1 = time.perf_counter()
-    mt_runs = 0
+    mt_times = []
     while time.perf_counter() - t1 < max(1.0, seconds / 5):
+        r0 = time.perf_counter()
         O.gemm_w4a8_mt(aq, bq, wtype, threads)
-        mt_runs += 1
-    per_mt = (time.perf_counter() - t1) / mt_runs
+        mt_times.append(time.perf_counter() - r0)
+    mt_times.sort()
+    per_mt = mt_times[len(mt_times) // 2]
     flops = 2.0 * m * n * k
+    model = cpu_model()
     return ({"value": flops / per / 1e12, "unit": "TFLOPS", "cores": 1, "kind": "port",
-             "ms_per_gemv": per * 1e3,
+             "ms_per_gemv": per * 1e3, "ms_p10_p90": [times[runs // 10] * 1e3, times[(9 * runs) // 10] * 1e3],
+             "cpu": model,
              "sample": f"oracle/qg_oracle.c gemm_w4a8 (restates include/gemm_reference.h:175-222), "
-                       f"M={m} N={n} K={k}, {runs} runs in {el:.1f} s, 1 thread, step4 srand(42) inputs"},
+                       f"M={m} N={n} K={k}, median of {runs} runs in {el:.1f} s, 1 thread pinned to core "
+                       f"{core}, step4 srand(42) inputs"},
             {"value": flops / per_mt / 1e12, "unit": "TFLOPS", "cores": threads, "ms_per_gemv": per_mt * 1e3,
-             "sample": f"row-partitioned over {threads} threads, {mt_runs} runs"})
+             "cpu": model, "sample": f"row-partitioned over {threads} threads, median of {len(mt_times)} runs"})
 
 
 def main() -> None:
@@ -249,6 +278,23 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # ---- per-step distribution (median, p10, p90), in its own pass after the
+    #      timed region: HIP events around each step's launches on the launch stream
+    step_pct = None
+    if graphs is not None:
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(max(args.steps, 10))]
+        for i, (ea, eb) in enumerate(evs):
+            ea.record()
+            graphs[i % 2].replay()
+            eb.record()
+        torch.cuda.synchronize()
+        per = sorted(ea.elapsed_time(eb) * 1e3 / G for ea, eb in evs)
+        q = lambda f: round(per[min(len(per) - 1, int(f * len(per)))], 3)
+        step_pct = {"p10": q(0.1), "p50": q(0.5), "p90": q(0.9), "steps": len(per),
+                    "note": "us per launch, per step (HIP events around each step's graph replay)"}
+
     # ---- the same G GEMVs as ONE strided-batched launch (qg_gemm_w4a8_strided_batched): the
     #      per-launch dispatch cost is paid once per step instead of once per GEMV
     batched_us = None
@@ -346,7 +392,8 @@ def main() -> None:
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "us_per_launch": round(launch_us, 3), "bytes_per_launch": launch_bytes,
                          "timing": "HIP events on the launch stream over the timed graph replays, "
-                                   "per launch incl. its dispatch boundary"},
+                                   "per launch incl. its dispatch boundary",
+                         "per_step": step_pct},
             "batched": None if batched_us is None else {
                 "us_per_gemv": round(batched_us, 3),
                 "tflops": round(flops_per_gemv / world / batched_us / 1e6, 3),
