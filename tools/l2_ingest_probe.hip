@@ -120,6 +120,45 @@ __global__ __launch_bounds__(512) void mmq_pat(const unsigned char* __restrict__
     out[blockIdx.x * 512 + threadIdx.x] = reinterpret_cast<unsigned*>(lds)[threadIdx.x];
 }
 
+// The register-weight alternative for the M=32 prefill: workgroup x reads weight rows 32x..32x+31
+// (2304 B each; two workgroups per row slice, as the 2 token tiles), wave w takes K-stages w, w+8, ..
+// of 4 blocks; per stage and row tile a lane (r = lane & 15, q = lane >> 4) loads what the i8 MFMA
+// operand needs: per block pair an 8-B load at 4q and a 4-B load at 20 + 4q (+ the d dwords when
+// D), NB stages in flight. XOR-reduced, one store per lane. Weights cold (rotated over > 600 MB).
+template <int NB, bool D>
+__global__ __launch_bounds__(512) void rw_pat(const unsigned char* __restrict__ W, unsigned* out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    const int x = blockIdx.x & 127;
+    unsigned acc = 0;
+    const unsigned char* rows[2] = {W + (long)(32 * x + r) * 2304, W + (long)(32 * x + 16 + r) * 2304};
+    for (int h0 = wave; h0 < 32; h0 += 8 * NB) {
+        unsigned v[NB][2][2][D ? 5 : 3];
+#pragma unroll
+        for (int s = 0; s < NB; ++s) {
+            const int h = min(h0 + 8 * s, 31);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const unsigned* pp = reinterpret_cast<const unsigned*>(rows[i] + h * 72 + 36 * p);
+                    const uint2 a = *reinterpret_cast<const uint2*>(pp + q);
+                    v[s][i][p][0] = a.x; v[s][i][p][1] = a.y;
+                    v[s][i][p][2] = pp[5 + q];
+                    if constexpr (D) { v[s][i][p][3] = pp[0]; v[s][i][p][4] = pp[4]; }
+                }
+        }
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int k = 0; k < (D ? 5 : 3); ++k) acc ^= v[s][i][p][k];
+    }
+    out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 __global__ void empty(unsigned* out) {
     if (threadIdx.x == 1023 && blockIdx.x == 100000) out[0] = 1;
 }
@@ -178,6 +217,21 @@ int main() {
             CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             timeit(nm, [&](int i) { hipLaunchKernelGGL(kern, dim3(256), dim3(512), lds, st, ds[i % R], A32, out); });
         };
+        // cold weights for the register-weight patterns: rotate over > 600 MB of 9.4-MB weight sets
+        const int RW = 72;
+        std::vector<unsigned char*> wc(RW);
+        for (auto& p : wc) { CK(hipMalloc(&p, 9437184)); CK(hipMemset(p, 0x21, 9437184)); }
+        if (0) timeit("rw_pat NB=1 (cold)", [&](int i) { hipLaunchKernelGGL((rw_pat<1, false>), dim3(256), dim3(512), 0, st, wc[i % RW], out); });
+        if (0) timeit("rw_pat NB=2 (cold)", [&](int i) { hipLaunchKernelGGL((rw_pat<2, false>), dim3(256), dim3(512), 0, st, wc[i % RW], out); });
+        if (0) timeit("rw_pat NB=4 (cold)", [&](int i) { hipLaunchKernelGGL((rw_pat<4, false>), dim3(256), dim3(512), 0, st, wc[i % RW], out); });
+        if (0) timeit("rw_pat NB=2 +d loads (cold)", [&](int i) { hipLaunchKernelGGL((rw_pat<2, true>), dim3(256), dim3(512), 0, st, wc[i % RW], out); });
+        timeit("mmq_pat SB=4 NB=2 weights cold", [&](int i) { hipLaunchKernelGGL((mmq_pat<4, 2>), dim3(256), dim3(512), 8 * 2 * 5 * 1024, st, wc[i % RW], A32, out); });
+        timeit("mmq_pat SB=4 NB=4 weights cold", [&](int i) { hipLaunchKernelGGL((mmq_pat<4, 4>), dim3(256), dim3(512), 8 * 4 * 5 * 1024, st, wc[i % RW], A32, out); });
+        timeit("mmq_pat SB=8 NB=2 weights cold", [&](int i) { hipLaunchKernelGGL((mmq_pat<8, 2>), dim3(256), dim3(512), 8 * 2 * 9 * 1024, st, wc[i % RW], A32, out); });
+        timeit("mmq_pat SB=16 NB=1 weights cold", [&](int i) { hipLaunchKernelGGL((mmq_pat<16, 1>), dim3(256), dim3(512), 8 * 1 * 18 * 1024, st, wc[i % RW], A32, out); });
+        timeit("coalesced sh 73.7K + wt 73.7K/2 cold", [&](int i) { hipLaunchKernelGGL(rd<4>, dim3(G), dim3(512), 0, st, (const u32x4*)A32, (const u32x4*)wc[i % RW], 4608, 4608, out, 128); });
+        timeit("coalesced wt 73.7K/2 only cold", [&](int i) { hipLaunchKernelGGL(rd<4>, dim3(G), dim3(512), 0, st, (const u32x4*)A32, (const u32x4*)wc[i % RW], 0, 4608, out, 128); });
+        timeit("coalesced wt 36.9K (x1) only cold", [&](int i) { hipLaunchKernelGGL(rd<4>, dim3(G), dim3(512), 0, st, (const u32x4*)A32, (const u32x4*)wc[i % RW], 0, 2304, out, 256); });
         pat("mmq_pat SB=4  NB=2", mmq_pat<4, 2>, 8 * 2 * 5 * 1024);
         pat("mmq_pat SB=4  NB=4", mmq_pat<4, 4>, 8 * 4 * 5 * 1024);
         pat("mmq_pat SB=8  NB=2", mmq_pat<8, 2>, 8 * 2 * 9 * 1024);
