@@ -94,7 +94,7 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // conflicts).
 template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4> struct mmq_geom {
     using T = wfmt<F>;
-    static_assert(SB == 4 || SB == 8, "4 or 8 blocks per stage");
+    static_assert(SB == 4 || SB == 8 || SB == 16, "4, 8 or 16 blocks per stage");
     static constexpr int RSB = SB * T::BB;                     // weight bytes per row per stage
     static constexpr int WPS = P16 ? 16 : 4;                   // weight DMA piece (bytes)
     static constexpr int RIMG = P16 && RSB % 16 != 0 ? RSB + 8 : RSB;  // row image bytes
@@ -117,7 +117,7 @@ template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4
     static constexpr int NACC = RT * TT * 4;                   // accumulators per lane
     // wave buffers; the end-of-kernel partial tiles reuse them (after a barrier)
     static constexpr size_t LDS = (size_t)W * (NB * BUF > NACC * 256 ? NB * BUF : NACC * 256);
-    static_assert(NB >= 2 && NB <= 4, "2..4 stage buffers per wave");
+    static_assert(NB >= 1 && NB <= 4, "1..4 stage buffers per wave");
     static_assert(LDS <= 160 * 1024, "LDS per workgroup");
     static_assert(OFF_A % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
     static_assert(RSB % 8 == 0, "stage segments are 8-B multiples");
