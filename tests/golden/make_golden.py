@@ -68,6 +68,7 @@ def w4a16_case(run, m, n, k, seed=42):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--force", action="store_true", help="rewrite fixtures that already exist")
     args = ap.parse_args()
 
     run_q4_0 = load_reference_fn(args.ref, "quant_gemm/w4a8_q4_0_q8_1_n4096_k4096.json")
@@ -85,11 +86,22 @@ def main() -> None:
     }
     cases["w4a16_q4_0_m2n16k256"] = w4a16_case(run_w4a16, 2, 16, 256)
     cases["w4a16_q4_0_m3n8k96"] = w4a16_case(run_w4a16, 3, 8, 96, seed=5)
+    # at the headline K = 4096: the srand(42) stream draws A then B, so these are the first rows
+    # of BASELINE configs[1] (M=1, N=4096) exactly; M=8 takes the prefill (MFMA) path on the GPU
+    cases["w4a8_q4_0_m1n8k4096"] = w4a8_case(run_q4_0, 1, 8, 4096, O.Q4_0)
+    cases["w4a8_q4_0_m8n4k4096"] = w4a8_case(run_q4_0, 8, 4, 4096, O.Q4_0)
+    cases["w4a8_q4_1_m1n4k4096"] = w4a8_case(run_q4_1, 1, 4, 4096, O.Q4_1)
+    cases["w4a16_q4_0_m1n4k4096"] = w4a16_case(run_w4a16, 1, 4, 4096)
     for name, d in cases.items():
-        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
+        path = os.path.join(HERE, f"{name}.npz")
+        if os.path.exists(path) and not args.force:
+            continue  # committed fixtures stay byte-identical unless regenerated on purpose
+        np.savez_compressed(path, **d)
         print(f"{name}: C[0,:4]={d['c_ref'].ravel()[:4]}")
 
     # Q8_1 quantizer: the definition's own bytes for 16 rows x 4 blocks of the step4 A stream.
+    if os.path.exists(os.path.join(HERE, "quantize_q8_1_m16k128.npz")) and not args.force:
+        return
     a, _ = O.fill_uniform_step4(16, 0, 128, 42)
     blocks = np.stack([np.frombuffer(quant_q8_1(a[r, 32 * j:32 * j + 32]), np.uint8)
                        for r in range(16) for j in range(4)]).reshape(16, 4, 36)
