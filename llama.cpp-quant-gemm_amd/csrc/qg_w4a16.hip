@@ -29,13 +29,19 @@ template <int F, int BPL> struct w16_geom {
     static_assert(UB % 4 == 0, "whole-dword units");
 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // Exact float value of weight element j (0..3) of decoded dword x: q - 8 (Q4_0), q (Q8_0).
 template <int F> __device__ __forceinline__ float w16_elem(uint32_t x, int j) {
     if constexpr (F == FMT_Q8_0) return (float)(int)(int8_t)(x >> (8 * j));
     else return (float)((x >> (8 * j)) & 0xFFu) - 8.0f;
 }
 
-template <int F, int MT, int BPL, int LPR, int WGS>
+// ONEU (MT == 1, K <= 32 * BPL * LPR): every lane owns at most one unit, so there is no unit loop;
+// the lane's activation records are read into registers right after the staging barrier, before
+// its weights land (as the W4A8 GEMV's PRE / ONEU, qg_gemv_kernel.hpp), leaving only VALU work
+// once the weight bytes arrive.
+template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                        float* __restrict__ C, int M, int N, int K, long ldc_m,
                                                        long ldc_n, long sA, long sC) {
@@ -93,7 +99,41 @@ __global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
 
-    const int iters = (U + LPR - 1) / LPR;
+    // one block of this lane's unit against its activation records (registers or LDS)
+    auto block_dot = [&](const wblock& wb, const float4* a4) {
+        // element pairs on the packed-f32 ALU: byte -> f32 (v_cvt_f32_ubyte*), minus the offset as
+        // one v_pk_add per pair (Q8_0: sign bit flipped first, offset 128), one v_pk_fma per pair
+        // into two pair accumulators; exact weight values
+        constexpr float OFF = F == FMT_Q8_0 ? -128.0f : -8.0f;
+        f32x2 p0 = {0.0f, 0.0f}, p1 = {0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t x = F == FMT_Q8_0 ? wb.q[i] ^ 0x80808080u : wb.q[i];
+            const f32x2 w0 = f32x2{(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)} + f32x2{OFF, OFF};
+            const f32x2 w1 = f32x2{(float)((x >> 16) & 0xFFu), (float)(x >> 24)} + f32x2{OFF, OFF};
+            const float4 a = a4[i];
+            p0 = __builtin_elementwise_fma(f32x2{a.x, a.y}, w0, p0);
+            p1 = __builtin_elementwise_fma(f32x2{a.z, a.w}, w1, p1);
+        }
+        return (p0.x + p1.x) + (p0.y + p1.y);
+    };
+    if constexpr (ONEU) {
+        static_assert(MT == 1, "one activation row");
+        const int u = lir;
+        float4 pre[BPL][8];
+        if (u < U) {
+#pragma unroll
+            for (int bi = 0; bi < BPL; ++bi)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) pre[bi][i] = *reinterpret_cast<const float4*>(lds_f + u * G::REC_DW + bi * 32 + 4 * i);
+            __builtin_amdgcn_sched_barrier(0);
+            static_for<BPL>([&](auto BI) {
+                const wblock wb = decode_block<F, decltype(BI)::value>(cur);
+                acc[0] = __builtin_fmaf(wb.d, block_dot(wb, pre[decltype(BI)::value]), acc[0]);
+            });
+        }
+    }
+    const int iters = ONEU ? 0 : (U + LPR - 1) / LPR;
     for (int j = 0; j < iters; ++j) {
         const int u = lir + j * LPR;
         uint32_t nxt[G::UDW];
@@ -102,24 +142,11 @@ __global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__
             static_for<BPL>([&](auto BI) {
                 constexpr int bi = decltype(BI)::value;
                 const wblock wb = decode_block<F, bi>(cur);
-                float w[32];
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) w[4 * i + e] = w16_elem<F>(wb.q[i], e);
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     if (m < M) {
                         const float* rec = lds_f + (m * U + u) * G::REC_DW + bi * 32;
-                        float s = 0.0f;
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            const float4 a = *reinterpret_cast<const float4*>(rec + 4 * i);
-                            s = __builtin_fmaf(a.x, w[4 * i], s);
-                            s = __builtin_fmaf(a.y, w[4 * i + 1], s);
-                            s = __builtin_fmaf(a.z, w[4 * i + 2], s);
-                            s = __builtin_fmaf(a.w, w[4 * i + 3], s);
-                        }
+                        const float s = block_dot(wb, reinterpret_cast<const float4*>(rec));
                         acc[m] = __builtin_fmaf(wb.d, s, acc[m]);
                     }
                 }
@@ -188,7 +215,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4a4_t __attribute__((ext_vector_type(4), aligned(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t hi16_pack(uint32_t lo_elem, uint32_t hi_elem) {
     return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // {lo_elem[31:16], hi_elem[31:16]}
@@ -578,13 +604,13 @@ constexpr size_t W16_LDS_MAX = 160 * 1024;
 
 template <int F, int BPL> size_t w16_lds(int mt, int K) { return (size_t)mt * (K / QK / BPL) * w16_geom<F, BPL>::REC_DW * 4; }
 
-template <int F, int MT, int BPL, int LPR, int WGS>
+template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU = false>
 hipError_t w16_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
     const int rows = g.M < MT ? g.M : MT;
     const size_t lds = w16_lds<F, BPL>(rows, g.K);
     const dim3 grid((g.N + RPB - 1) / RPB, (g.M + MT - 1) / MT);
-    auto kfn = w16_gemv_kernel<F, MT, BPL, LPR, WGS>;
+    auto kfn = w16_gemv_kernel<F, MT, BPL, LPR, WGS, ONEU>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -598,8 +624,12 @@ template <int F, int MT> hipError_t w16_launch_mt(const GemmArgs& g, hipStream_t
     const int nb = g.K / QK;
     // 2-block units, one row per wave, 1024-thread workgroups: half the per-wave work of the 4-block
     // shape (as the W4A8 GEMV, qg_gemv.hip)
-    if (MT <= 4 && nb % 2 == 0 && nb / 2 >= 64 && w16_lds<F, 2>(g.M < MT ? g.M : MT, g.K) <= W16_LDS_MAX)
+    if (MT <= 4 && nb % 2 == 0 && nb / 2 >= 64 && w16_lds<F, 2>(g.M < MT ? g.M : MT, g.K) <= W16_LDS_MAX) {
+        // K == 4096, Q4_0: one unit per lane (M=1 4.82 -> 4.61 us; Q8_0 measured no better)
+        if constexpr (MT == 1 && F == FMT_Q4_0)
+            if (nb / 2 <= 64) return w16_launch<F, 1, 2, 64, 1024, true>(g, st);
         return w16_launch<F, MT, 2, 64, 1024>(g, st);
+    }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return w16_launch<F, MT, 4, 32, 512>(g, st);
         return w16_launch<F, MT, 4, 4, 256>(g, st);
