@@ -20,10 +20,14 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     // (a strided batch uses the same shape, so its outputs equal the single launches' bit for bit;
     // the fused-quantization prologue is repeated per workgroup, so it keeps 16 rows per workgroup,
     // with the same per-row summation order)
-    if (MT <= 4 && !SUMI && nb % 2 == 0 && nb / 2 >= 64) {
-        if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
-            return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
-        return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN>(g, st);
+    if constexpr (MT <= 4 && !SUMI) {
+        if (nb % 2 == 0 && nb / 2 >= 64) {
+            if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
+                return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
+            // activation records preloaded into registers for M <= 4 (tools/gemv_pre_probe.hip,
+            // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
+            return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN, false, true>(g, st);
+        }
     }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);

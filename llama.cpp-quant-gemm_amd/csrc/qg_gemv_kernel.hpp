@@ -389,8 +389,9 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
     const bool one = g.K / QK / BPL <= LPR;
+    // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4)
     auto kfn = one ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
-                   : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, false>;
+                   : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE && (MT <= 2), false>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
