@@ -334,3 +334,51 @@ def test_allquants_full_size(O, qg, t, bound):
     c = host(qg.gemm_w4a8(dev(aq), dev(bq), 1, 4096, 4096, t))
     assert_close_to_oracle(O, c, aq, bq, t)
     assert O.nmse(c, O.gemm_fp32(a, b)) <= bound
+
+
+# ------------------------------------------------------------------------------- full-size properties
+def test_row_shards_bit_identical_full_size(qg):
+    """BASELINE configs[4] on one GPU: the 8 row shards of N=32000 (4000 rows each, as the 8 ranks
+    compute them, quant_gemm.sharded.shard_rows) reassemble the full GEMV bit for bit — rows are
+    independent, so the multi-GPU split changes no output bit."""
+    import torch
+    from quant_gemm.sharded import shard_rows
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(11)
+    n, k = 32000, 4096
+    aq = qg.quantize_q8_1(torch.rand((1, k), generator=gen, device="cuda") * 2 - 1)
+    bq = qg.quantize_q4_0(torch.rand((n, k), generator=gen, device="cuda") * 2 - 1)
+    full = qg.gemm_w4a8(aq, bq, 1, n, k)
+    parts = []
+    for r in range(8):
+        s0, s1 = shard_rows(n, 8, r)
+        parts.append(qg.gemm_w4a8(aq, bq[s0:s1], 1, s1 - s0, k))
+    assert torch.equal(torch.cat(parts, dim=1), full)
+
+
+@pytest.mark.parametrize("t", WTYPES)
+def test_batched_equals_single_full_size(qg, t):
+    """A strided batch of 6 full-size GEMVs (M=1, N=K=4096) equals six single launches bit for bit."""
+    import torch
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(12 + t)
+    k, n, B = 4096, 4096, 6
+    aq = torch.stack([qg.quantize_q8_1(torch.rand((1, k), generator=gen, device="cuda") * 2 - 1) for _ in range(B)])
+    bq = torch.stack([qg.quantize(torch.rand((n, k), generator=gen, device="cuda") * 2 - 1, t) for _ in range(B)])
+    cb = qg.gemm_w4a8_batched(aq, bq, 1, n, k, t)
+    for i in range(B):
+        assert torch.equal(cb[i], qg.gemm_w4a8(aq[i], bq[i], 1, n, k, t))
+
+
+def test_weight_major_is_transpose_full_size(qg):
+    """BASELINE configs[2] (M=32 prefill): the reference's weight-major entry (gemm_q4_0_q8_1,
+    out[Mw][Ntok]) is the activation-major product transposed, bit for bit."""
+    import torch
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(13)
+    m, n, k = 32, 4096, 4096
+    aq = qg.quantize_q8_1(torch.rand((m, k), generator=gen, device="cuda") * 2 - 1)
+    bq = qg.quantize_q4_0(torch.rand((n, k), generator=gen, device="cuda") * 2 - 1)
+    c = qg.gemm_w4a8(aq, bq, m, n, k)
+    w = qg.gemm_q4_0_q8_1(bq, aq, n, m, k)
+    assert torch.equal(w.T, c)
