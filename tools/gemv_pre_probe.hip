@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "qg_gemv_kernel.hpp"
+#include "../../include/qg/qg.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -74,5 +75,11 @@ int main() {
         }
     }
     run("MT1 PRE (product)", 1, gemv_launch<FMT_Q4_0, 1, 2, 64, 1024, false, AIN_Q8_1, false, true>);
+    for (int M : {5, 8}) {
+        run("C-ABI auto (MMQ)", M, [](const GemmArgs& g, hipStream_t s) { return qg_gemm_w4a8(g.A, g.B, g.C, g.M, g.N, g.K, QG_TYPE_Q4_0, s) == 0 ? hipSuccess : hipErrorUnknown; });
+        run("MT8 no PRE 1024", M, gemv_launch<FMT_Q4_0, 8, 2, 64, 1024, false, AIN_Q8_1, false, false>);
+        run("MT8 PRE 512", M, gemv_launch<FMT_Q4_0, 8, 2, 64, 512, false, AIN_Q8_1, false, true>);
+        run("MT8 no PRE 512", M, gemv_launch<FMT_Q4_0, 8, 2, 64, 512, false, AIN_Q8_1, false, false>);
+    }
     return 0;
 }
