@@ -141,7 +141,7 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // per output tile) sums the KS partials in slice order (deterministic: the same order whichever
 // workgroup arrives last) and re-arms the counter to 0 for the next launch.
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1>
+          int KS = 1, bool EPI2 = false>
 __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
@@ -277,6 +277,135 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     // 4 x RT x TT MFMAs back to back, then the VALU epilogues (block b's results are read behind
     // the later blocks' MFMAs and epilogues, plus an explicit wait for the matrix pipe: reading
     // them with only the wait states hipcc inserts gave wrong sums, tools/mmq_debug.hip).
+    // EPI2 (!SUMI): the scale arithmetic moves onto the matrix pipe. Per block, one
+    // v_mfma_f32_16x16x16_f16 forms the outer product d_w (x) d_a (k-slot 0 only: exact f16 x f16 in
+    // f32) in the accumulator layout, so the VALU epilogue is sumi = cf - 1.5*2^23 (exact) and
+    // acc += dd * sumi — one packed op per element instead of two; the compensation term
+    // sum_b X[n][b] s_a[m][b] (X = d_w, or m_w for Q4_1 / Q5_1) is accumulated over each stage's
+    // 4 blocks by one more MFMA per tile into c2 and added once at the end (x -8 / -16 / +1).
+    // Each lane reads only its own row's d_w (and m_w): 1 LDS read per row tile and block instead
+    // of 4. Within the fp32 summation-order bound of the parity tests (the per-term rounding
+    // differs from the reference's d_w * (d_a * sumi - c * s_a)).
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr bool HAS_S = F != FMT_Q8_0;
+    constexpr float CFAC = F == FMT_Q4_0 ? -8.0f : F == FMT_Q5_0 ? -16.0f : 1.0f;
+    f32x4v c2[EPI2 ? G::RT : 1][EPI2 ? TT : 1];
+    if constexpr (EPI2) {
+#pragma unroll
+        for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t) c2[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    auto h4 = [](unsigned long v) { return __builtin_bit_cast(f16x4, v); };
+    auto compute4_e2 = [&](uint8_t* buf, int h, int sh, auto SUB) {
+        constexpr int b0 = 4 * decltype(SUB)::value;
+        long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
+        uint32_t wdb[MMQ_SB][G::RT], wmb[MMQ_SB][G::RT], adb[MMQ_SB][TT];
+        const bool q0 = q == 0;
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+            constexpr int o = (b0 + b) * T::BB;
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i) {
+                const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
+                uint32_t lo, hi;
+                if constexpr (T::Q8) {
+                    lo = lds32<o + T::QS>(wr + 4 * q);
+                    hi = lds32<o + T::QS + 16>(wr + 4 * q);
+                } else {
+                    const uint32_t v = lds32<o + T::QS>(wr + 4 * q);
+                    lo = v & 0x0F0F0F0Fu;
+                    hi = (v >> 4) & 0x0F0F0F0Fu;
+                }
+                if constexpr (T::QH >= 0) {
+                    const uint32_t qh = lds32<o + T::QH>(wr);
+                    lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
+                    hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
+                }
+                afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
+                wdb[b][i] = u16(wr + o);
+                if constexpr (HAS_M) wmb[b][i] = u16(wr + o + T::MOFF);
+            }
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * G::ASTR + (b0 + b) * Q8_1_BYTES;
+                const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
+                const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
+                bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
+                adb[b][t] = *reinterpret_cast<const uint32_t*>(ar);  // f16 d_a | f16 s_a << 16
+            }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4v dd[MMQ_SB][G::RT][TT];
+        v4i cc[MMQ_SB][G::RT][TT];
+        const f32x4v z4 = {0.f, 0.f, 0.f, 0.f};
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+                    dd[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                        h4(q0 ? (unsigned long)(wdb[b][i] & 0xFFFFu) : 0ul),
+                        h4(q0 ? (unsigned long)(adb[b][t] & 0xFFFFu) : 0ul), z4, 0, 0, 0);
+        });
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i)
+                    cc[b][i][t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(afrag[b][i], bfrag[b][t], bias, 0, 0, 0);
+        });
+        if constexpr (HAS_S) {
+            // k-slots 0..3 = the sub-stage's 4 blocks (lanes q = 0 only)
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i) {
+                const uint32_t* X = HAS_M ? wmb[0] : wdb[0];
+                (void)X;
+                uint32_t x01, x23;
+                if constexpr (HAS_M) {
+                    x01 = __builtin_amdgcn_perm(wmb[1][i], wmb[0][i], 0x05040100u);
+                    x23 = __builtin_amdgcn_perm(wmb[3][i], wmb[2][i], 0x05040100u);
+                } else {
+                    x01 = __builtin_amdgcn_perm(wdb[1][i], wdb[0][i], 0x05040100u);
+                    x23 = __builtin_amdgcn_perm(wdb[3][i], wdb[2][i], 0x05040100u);
+                }
+                const unsigned long xa = q0 ? (((unsigned long)x23 << 32) | x01) : 0ul;
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    const uint32_t s01 = __builtin_amdgcn_perm(adb[1][t], adb[0][t], 0x07060302u);
+                    const uint32_t s23 = __builtin_amdgcn_perm(adb[3][t], adb[2][t], 0x07060302u);
+                    const unsigned long sb = q0 ? (((unsigned long)s23 << 32) | s01) : 0ul;
+                    c2[i][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(h4(xa), h4(sb), c2[i][t], 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<MMQ_SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+#pragma unroll
+            for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int e = 0; e < 4; e += 2) {
+                        const f32x2 sm = f32x2{__int_as_float(cc[b][i][t][e]), __int_as_float(cc[b][i][t][e + 1])} -
+                                         f32x2{MMQ_BIAS_F, MMQ_BIAS_F};  // exact: sumi
+                        float* a = &acc[(i * TT + t) * 4 + e];
+                        const f32x2 r = __builtin_elementwise_fma(f32x2{dd[b][i][t][e], dd[b][i][t][e + 1]}, sm,
+                                                                  f32x2{a[0], a[1]});
+                        a[0] = r.x;
+                        a[1] = r.y;
+                    }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        (void)h;
+    };
+
     auto compute4 = [&](uint8_t* buf, int h, int sh, auto SUB) {
         constexpr int b0 = 4 * decltype(SUB)::value;  // first block of this 4-block sub-stage
         blk_t blk[MMQ_SB];
@@ -349,7 +478,10 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     };
 
     auto compute = [&](uint8_t* buf, int h, int sh) {
-        static_for<SB / 4>([&](auto SUB) { compute4(buf, h, sh, SUB); });
+        if constexpr (EPI2 && !SUMI && ABL == 0)
+            static_for<SB / 4>([&](auto SUB) { compute4_e2(buf, h, sh, SUB); });
+        else
+            static_for<SB / 4>([&](auto SUB) { compute4(buf, h, sh, SUB); });
     };
 
     // this wave's stages h = wave + k W (k < nst), up to NB of them in flight. ROT: the workgroups
@@ -380,6 +512,15 @@ __global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__
     }
     MMQ_STAMP(3);
 
+    if constexpr (EPI2 && !SUMI && HAS_S) {
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // the last compensation MFMAs retired
+#pragma unroll
+        for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[(i * TT + t) * 4 + e] = __builtin_fmaf(CFAC, c2[i][t][e], acc[(i * TT + t) * 4 + e]);
+    }
     if constexpr (!SUMI) {
         // fixed-order sum of the W partial tiles, in the wave buffers once every wave is done
         float* red = reinterpret_cast<float*>(smem);
@@ -465,11 +606,11 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
 }
 
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1>
+          int KS = 1, bool EPI2 = false>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK, KS);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2>;
     unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;
     float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
     if (G::LDS > 64 * 1024) {

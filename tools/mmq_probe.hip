@@ -33,9 +33,8 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     struct S { int F, M, N, K; };
-    const S shapes[] = {{FMT_Q4_0, 32, 4096, 4096}, {FMT_Q4_0, 16, 4096, 4096}, {FMT_Q4_0, 64, 4096, 4096},
-                        {FMT_Q4_0, 32, 11008, 4096}, {FMT_Q4_0, 32, 4096, 11008},
-                        {FMT_Q4_0, 16, 4096, 14336}};
+    const S shapes[] = {{FMT_Q4_0, 32, 4096, 4096}, {FMT_Q4_0, 8, 4096, 4096}, {FMT_Q4_0, 64, 4096, 4096},
+                        {FMT_Q4_0, 128, 4096, 4096}, {FMT_Q4_0, 512, 4096, 4096}};
     for (const S& s : shapes) {
         const int nb = s.K / 32, bb = block_bytes(s.F);
         const long wbytes = (long)s.N * nb * bb;
@@ -88,13 +87,14 @@ int main() {
         VA(16, 2, 8, 4, "abl4 wt-only bn16 tt2 w8")
 #define VS(BN, TT, W, NB, SB, ABL, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB, SB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB, ABL, false, SB>(g, st) : hipErrorInvalidValue; }});
-        VS(32, 1, 16, 1, 8, 0, "sb8 w16 nb1")
-        VS(32, 1, 8, 1, 16, 0, "sb16 w8 nb1")
-        VS(32, 1, 8, 2, 8, 0, "sb8 w8 nb2")
-        VS(32, 1, 16, 1, 8, 1, "abl1 sb8 w16 nb1")
-        VS(32, 1, 8, 1, 16, 1, "abl1 sb16 w8 nb1")
-        VS(16, 1, 8, 1, 16, 0, "sb16 bn16 w8 nb1")
 #undef VS
+#define VE(BN, TT, W, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
+        return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, 2>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, 2, 0, false, 4, 1, true>(g, st) : hipErrorInvalidValue; }});
+        VE(32, 1, 8, "EPI2 bn32 tt1 w8")
+        VE(16, 1, 8, "EPI2 bn16 tt1 w8")
+        VE(32, 2, 8, "EPI2 bn32 tt2 w8")
+        VE(32, 2, 4, "EPI2 bn32 tt2 w4")
+#undef VE
 #undef VA
 #undef VN
 #undef V
