@@ -19,12 +19,13 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
     return mmq_shape_ok<F, BN, TT, W, true>(g) || mmq_shape_ok<F, BN, TT, W, false>(g);
 }
 
-// 16-token tiles (M <= 32) use the MFMA-assisted epilogue (EPI2, qg_mmq_kernel.hpp):
-// profiles/r01_tuning/mmq_probe_epi2.txt — M=32 7.61 -> 7.39 us, M=8 5.56 -> 5.44 us; the 32-token
-// tiles of M > 32 gain nothing from it and keep the VALU epilogue
+// The MFMA-assisted epilogue (EPI2, qg_mmq_kernel.hpp) for the 8-wave configurations:
+// profiles/r01_tuning/mmq_probe_epi2.txt, mmq_probe_disp.txt — M=8 5.56 -> 5.44 us, M=32 7.61 ->
+// 7.39 us, M=48 10.17 -> 9.80 us, M=64 10.35 -> 10.19 us, M=128 flat; the 4-wave 32-token tiles of
+// large M run slower with it (register pressure) and keep the VALU epilogue
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16>(g, st);
-    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, TT == 1>(g, st);
+    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, W == 8>(g, st);
 }
 
 template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hipStream_t st) {
