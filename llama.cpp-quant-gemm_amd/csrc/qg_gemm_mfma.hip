@@ -36,14 +36,20 @@ inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.
 
 inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 512; }
 
+// 128 < M <= 384 beyond the few-tiles grids: 16-token tiles with the MFMA epilogue
+// (profiles/r01_tuning/mmq_probe_large.txt: M=256 31.0 -> 28.6 us; M >= 512 keeps 32 x 32 tiles)
+inline bool mid_m(const GemmArgs& g) { return g.M <= 384; }
+
 template <int F> bool ok_f(const GemmArgs& g) {
     if (g.M <= 32) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);
-    return few_tiles(g) ? ok_cfg<F, 32, 2, 8>(g) : ok_cfg<F, 32, 2, 4>(g);
+    if (few_tiles(g)) return ok_cfg<F, 32, 2, 8>(g);
+    return mid_m(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 32, 2, 4>(g);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 32) return wide_rows(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 16, 1, 8>(g, st);
-    return few_tiles(g) ? run_cfg<F, 32, 2, 8>(g, st) : run_cfg<F, 32, 2, 4>(g, st);
+    if (few_tiles(g)) return run_cfg<F, 32, 2, 8>(g, st);
+    return mid_m(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 32, 2, 4>(g, st);
 }
 }  // namespace
 

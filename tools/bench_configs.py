@@ -28,7 +28,7 @@ CONFIGS = [
     ("q4_0", 32, 4096, 4096), ("q4_0", 1, 32000, 4096), ("q4_0", 1, 4000, 4096),
     ("q4_0", 2, 4096, 4096), ("q4_0", 3, 4096, 4096), ("q4_0", 4, 4096, 4096),
     ("q4_0", 8, 4096, 4096), ("q4_0", 1, 4096, 14336), ("q4_0", 2, 4096, 14336), ("q4_0", 64, 4096, 4096),
-    ("q4_0", 128, 4096, 4096), ("q4_0", 512, 4096, 4096),
+    ("q4_0", 128, 4096, 4096), ("q4_0", 256, 4096, 4096), ("q4_0", 512, 4096, 4096),
     ("q8_0", 1, 4096, 4096), ("q8_0", 32, 4096, 4096),          # W8A8
     ("w4a16", 1, 4096, 4096), ("w4a16", 4, 4096, 4096), ("w4a16", 32, 4096, 4096), ("w4a16", 512, 4096, 4096),
     ("w8a16", 1, 4096, 4096), ("w8a16", 32, 4096, 4096),
