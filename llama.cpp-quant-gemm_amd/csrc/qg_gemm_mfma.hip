@@ -19,13 +19,13 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
     return mmq_shape_ok<F, BN, TT, W, true>(g) || mmq_shape_ok<F, BN, TT, W, false>(g);
 }
 
-// The MFMA-assisted epilogue (EPI2, qg_mmq_kernel.hpp) for the 8-wave configurations:
-// profiles/r01_tuning/mmq_probe_epi2.txt, mmq_probe_disp.txt — M=8 5.56 -> 5.44 us, M=32 7.61 ->
-// 7.39 us, M=48 10.17 -> 9.80 us, M=64 10.35 -> 10.19 us, M=128 flat; the 4-wave 32-token tiles of
-// large M run slower with it (register pressure) and keep the VALU epilogue
+// The MFMA-assisted epilogue (EPI2, qg_mmq_kernel.hpp) in every configuration:
+// profiles/r01_tuning/mmq_probe_epi2.txt, mmq_probe_disp.txt, mmq_probe_lb.txt — M=8 5.56 -> 5.44
+// us, M=32 7.61 -> 7.39, M=64 10.35 -> 10.19, M=256 29.2 -> 27.1, M=512 58.3 -> 50.9, M=1024
+// 108.9 -> 96.5 (the 4-wave 32 x 32 tiles with the two-workgroups-per-CU register cap)
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16>(g, st);
-    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, W == 8>(g, st);
+    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true>(g, st);
 }
 
 template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hipStream_t st) {
@@ -36,20 +36,14 @@ inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.
 
 inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 512; }
 
-// 128 < M <= 384 beyond the few-tiles grids: 16-token tiles with the MFMA epilogue
-// (profiles/r01_tuning/mmq_probe_large.txt: M=256 31.0 -> 28.6 us; M >= 512 keeps 32 x 32 tiles)
-inline bool mid_m(const GemmArgs& g) { return g.M <= 384; }
-
 template <int F> bool ok_f(const GemmArgs& g) {
     if (g.M <= 32) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);
-    if (few_tiles(g)) return ok_cfg<F, 32, 2, 8>(g);
-    return mid_m(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 32, 2, 4>(g);
+    return few_tiles(g) ? ok_cfg<F, 32, 2, 8>(g) : ok_cfg<F, 32, 2, 4>(g);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
     if (g.M <= 32) return wide_rows(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 16, 1, 8>(g, st);
-    if (few_tiles(g)) return run_cfg<F, 32, 2, 8>(g, st);
-    return mid_m(g) ? run_cfg<F, 32, 1, 8>(g, st) : run_cfg<F, 32, 2, 4>(g, st);
+    return few_tiles(g) ? run_cfg<F, 32, 2, 8>(g, st) : run_cfg<F, 32, 2, 4>(g, st);
 }
 }  // namespace
 

@@ -142,7 +142,9 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // workgroup arrives last) and re-arms the counter to 0 for the next launch.
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
           int KS = 1, bool EPI2 = false>
-__global__ __launch_bounds__(W * 64) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+// (4-wave workgroups: at least two per CU, i.e. <= 256 VGPRs — without the cap the EPI2 form took
+// 320 and ran one workgroup per CU, 13 % slower at M=512 than with it)
+__global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
                                                      unsigned* __restrict__ cnt) {
