@@ -94,6 +94,7 @@ int main() {
         VE(16, 1, 8, "EPI2 bn16 tt1 w8")
         VE(32, 2, 8, "EPI2 bn32 tt2 w8")
         VE(32, 2, 4, "EPI2 bn32 tt2 w4")
+
 #undef VE
 #undef VA
 #undef VN
