@@ -6,9 +6,9 @@
 //  * M <= 32: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
 //    >= 256 workgroups (one per CU; fewer re-reads of the activations), else 16
 //    (M=32, N=4096: 32 rows x 2 token tiles = 256 WGs; M=8, N=4096: 16 rows = 256 WGs)
-//  * M  > 32: 32 rows x 32 tokens; 8 waves splitting K while that grid has <= 512 workgroups, else
-//    4 (profiles/r01_tuning/mmq_probe_p4.txt: M=64 10.3 us, M=128 17.5 us, M=512 58 us; the
-//    former 32 rows x 64 tokens took 13.6 / 21.7 / 76.6 us)
+//  * M  > 32: 32 rows x 32 tokens; 8 waves splitting K while that grid has <= 256 workgroups, else
+//    4 (two workgroups per CU under the kernel's register cap; mmq_probe_p4.txt, mmq_probe_mid.txt,
+//    mmq_probe_lb.txt: M=64 10.1 us, M=128 15.2 us, M=512 47 us with the MFMA-assisted epilogue)
 #include "qg_mmq_kernel.hpp"
 
 namespace qg {
@@ -34,7 +34,9 @@ template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hi
 
 inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
 
-inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 512; }
+// 8 waves per 32 x 32 tile only while that leaves <= 256 workgroups; beyond, 4-wave workgroups two
+// per CU (profiles/r01_tuning/mmq_probe_mid.txt: M=96 16.5 -> 14.2 us, M=128 17.3 -> 15.5 us)
+inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 256; }
 
 template <int F> bool ok_f(const GemmArgs& g) {
     if (g.M <= 32) return wide_rows(g) ? ok_cfg<F, 32, 1, 8>(g) : ok_cfg<F, 16, 1, 8>(g);

@@ -33,8 +33,8 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     struct S { int F, M, N, K; };
-    const S shapes[] = {{FMT_Q4_0, 256, 4096, 4096}, {FMT_Q4_0, 512, 4096, 4096}, {FMT_Q4_0, 1024, 4096, 4096},
-                        {FMT_Q4_0, 512, 11008, 4096}, {FMT_Q4_0, 512, 4096, 11008}};
+    const S shapes[] = {{FMT_Q4_0, 64, 4096, 4096}, {FMT_Q4_0, 96, 4096, 4096}, {FMT_Q4_0, 128, 4096, 4096},
+                        {FMT_Q4_0, 128, 11008, 4096}, {FMT_Q4_0, 128, 4096, 11008}};
     for (const S& s : shapes) {
         const int nb = s.K / 32, bb = block_bytes(s.F);
         const long wbytes = (long)s.N * nb * bb;
