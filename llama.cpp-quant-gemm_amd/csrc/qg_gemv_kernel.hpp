@@ -108,9 +108,8 @@ template <int OFF> __device__ __forceinline__ float mixmul_at(const uint32_t* w,
 //           of dword i), [11] initial accumulator bits 1.5*2^23 + 128*sum(h);
 //   bytes:  [0..7] qs;
 //   both:   [8] d_a, [9] c * s_a, [10] -1.5*2^23 * d_a (fp32).
-template <int F> __device__ __forceinline__ void make_act_record(const uint32_t (&b)[9], uint32_t* rec) {
+template <int F> __device__ __forceinline__ void build_act_record(const uint32_t* b, uint32_t (&r)[12]) {
     const float d = h2f(b[0] & 0xFFFFu), s = h2f(b[0] >> 16);
-    uint32_t r[12];
     if constexpr (gemv_planes<F>) {
         int sh = 0;
 #pragma unroll
@@ -129,6 +128,10 @@ template <int F> __device__ __forceinline__ void make_act_record(const uint32_t 
     r[8] = __float_as_uint(d);
     r[9] = __float_as_uint(gemv_cs<F> * s);
     r[10] = __float_as_uint(-(d * ACC_BIAS_F));
+}
+template <int F> __device__ __forceinline__ void make_act_record(const uint32_t (&b)[9], uint32_t* rec) {
+    uint32_t r[12];
+    build_act_record<F>(b, r);
     *reinterpret_cast<uint4*>(rec) = make_uint4(r[0], r[1], r[2], r[3]);
     *reinterpret_cast<uint4*>(rec + 4) = make_uint4(r[4], r[5], r[6], r[7]);
     *reinterpret_cast<uint4*>(rec + 8) = make_uint4(r[8], r[9], r[10], r[11]);
