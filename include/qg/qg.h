@@ -65,6 +65,10 @@ typedef enum {
 int qg_gemm_w4a8(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, qg_stream_t stream);
 int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, int algo,
                     qg_stream_t stream);
+/* As qg_gemm_w4a8_ex with an output row stride: C[m * ldc + n], ldc >= N floats (e.g. a rank's
+ * column slice of a wider buffer in the row-sharded multi-GPU path, quant_gemm/sharded.py). */
+int qg_gemm_w4a8_ldc(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int64_t ldc, int wtype,
+                     int algo, qg_stream_t stream);
 
 /* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
  * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of
@@ -79,12 +83,15 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * then scaled by d once). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
  * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
- * call outside stream capture (a captured first call runs without split-K, same results to fp32
- * summation order). qg_release_workspaces() frees them (after a device synchronize).
+ * call outside stream capture. Calls made during stream capture never use the library's
+ * workspace: they run without split-K (same results to fp32 summation order), so a graph holds
+ * no pointer the library may free. qg_release_workspaces() frees them (after a device synchronize).
  * The _ws forms take the caller's workspace instead (for graphs and multi-stream callers):
  * >= qg_gemm_w16_workspace_size(M, N, K) bytes (0: no split-K for this shape), 256-B aligned,
- * zeroed once before its first use — every call leaves it zeroed again; calls that may run
- * concurrently need distinct workspaces. A smaller or misaligned workspace is not used. */
+ * zeroed once before its first use. Its layout is shape-independent: a counter region that every
+ * call leaves zeroed again, then scratch partial tiles — so one workspace serves calls of any
+ * shapes on one stream. Calls that may run concurrently need distinct workspaces. A smaller or
+ * misaligned workspace is not used. */
 void qg_release_workspaces(void);
 size_t qg_gemm_w16_workspace_size(int M, int N, int K);
 int qg_gemm_w4a16_ws(const float* A, const void* B_q4_0, float* C, int M, int N, int K, void* workspace,
@@ -152,10 +159,18 @@ int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_st
 int qg_dequantize(int type, const void* x, float* y, int64_t k, qg_stream_t stream);
 int qg_dequantize_q4_0(const void* x, float* y, int64_t k, qg_stream_t stream);
 
-/* ---- parity hook: per-block int32 dots sumi[M][N][K/32] through the SAME decode path the
- * chosen algorithm uses (the reference's inner loop, include/gemm_reference.h:202-212). */
+/* ---- parity hook: per-block int32 dots sumi[M][N][K/32] (the reference's inner loop,
+ * include/gemm_reference.h:202-212), computed by the SAME kernel instantiation qg_gemm_w4a8_ex
+ * launches for this shape and algo (same unit loads, operand records / MFMA fragments and integer
+ * dot instructions); only the per-block fp32 epilogue is replaced by a store of the int32 dot.
+ * The fp32 terms themselves are checked against the oracle to its summation-order bound (the
+ * MFMA-assisted prefill epilogue rounds its scale products differently from the reference). */
 int qg_debug_sumi(const void* A_q8_1, const void* B, int32_t* sumi, int M, int N, int K, int wtype, int algo,
                   qg_stream_t stream);
+/* The kernel instantiation (family + template parameters + grid) that qg_gemm_w4a8_ex (sumi = 0)
+ * or qg_debug_sumi (sumi = 1) would launch for this shape on 256-B aligned buffers, as text;
+ * nothing is launched. The parity tests assert the two are the same kernel. */
+int qg_debug_config(int M, int N, int K, int wtype, int algo, int sumi, char* buf, size_t len);
 
 /* ---- ggml-facing adapter (include/llama_adapter.h:49-76, declared but never defined there) ----
  * A minimal ggml_tensor view: ne[0] = K (contiguous), ne[1] = rows; nb[] byte strides.

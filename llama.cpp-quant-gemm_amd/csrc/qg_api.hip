@@ -3,7 +3,9 @@
 // No host synchronisation: every entry point validates, picks a kernel family and enqueues on the
 // caller's stream, so callers may capture it into a hipGraph. The one allocation is the split-K
 // workspace of the W4A16 / W8A16 prefill (stream_workspace below): made once per (device, stream)
-// outside capture; a captured first call runs the kernel without split-K instead.
+// outside capture and never used by a captured call (which runs the kernel without split-K).
+#include <stdarg.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -25,14 +27,18 @@ std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_ws;
 void* stream_workspace(hipStream_t st, size_t bytes) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    auto& e = g_ws[{dev, st}];
-    if (e.first && e.second >= bytes) return e.first;
+    // Never hand the library's buffer to a stream capture: a graph would keep its raw pointer,
+    // and a later eager call that grows the buffer (or qg_release_workspaces) would free it under
+    // the graph. Captured calls run without split-K; graphs pass their own workspace
+    // through the _ws entry points.
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
         (void)hipGetLastError();
         return nullptr;
     }
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto& e = g_ws[{dev, st}];
+    if (e.first && e.second >= bytes) return e.first;
     const size_t sz = std::max(bytes, (size_t)4 << 20);
     void* p = nullptr;
     if (hipMalloc(&p, sz) != hipSuccess) {
@@ -50,6 +56,14 @@ void* stream_workspace(hipStream_t st, size_t bytes) {
     }
     e = {p, sz};
     return p;
+}
+
+void describe_kernel(const GemmArgs& g, const char* fmt, ...) {
+    if (!g.describe || g.describe_len == 0) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g.describe, g.describe_len, fmt, ap);
+    va_end(ap);
 }
 
 void release_workspaces() {
@@ -95,7 +109,8 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     if (g.batch < 0) return QG_ERR_INVALID_ARG;
     if (g.batch == 0) return QG_OK;
     if (g.batch > 1 && (((uintptr_t)g.sB & 1) != 0 || (g.sA & 3) != 0)) return QG_ERR_ALIGN;
-    if (algo == QG_ALGO_AUTO) algo = select_algo(g);
+    const bool auto_algo = algo == QG_ALGO_AUTO;
+    if (auto_algo) algo = select_algo(g);
     if (algo == QG_ALGO_GEMV) {
         if (!gemv_eligible(g) || (g.batch > 1 && (g.sB % 16 != 0))) {
             if (g.batch == 1) return QG_ERR_UNSUPPORTED;
@@ -106,16 +121,30 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
         }
     }
     // MFMA and generic kernels take one product per launch: enqueue the batch item by item.
-    for (int i = 0; i < g.batch; ++i) {
+    auto item = [&](int i) {
         GemmArgs gi = g;
         gi.batch = 1;
         gi.A = (const uint8_t*)g.A + (long)i * g.sA;
         gi.B = (const uint8_t*)g.B + (long)i * g.sB;
         if (g.C) gi.C = g.C + (long)i * g.sC;
+        return gi;
+    };
+    // Every item is checked before the first is enqueued (a batch stride can break the MFMA
+    // kernel's 16-B alignment for later items only): an explicit MFMA request fails with nothing
+    // launched, an automatic choice falls back to the generic kernel for the whole batch.
+    if (algo == QG_ALGO_MFMA) {
+        bool all_ok = true;
+        for (int i = 0; i < g.batch && all_ok; ++i) all_ok = mfma_eligible(item(i));
+        if (!all_ok) {
+            if (!auto_algo) return QG_ERR_UNSUPPORTED;
+            algo = QG_ALGO_GENERIC;
+        }
+    }
+    for (int i = 0; i < g.batch; ++i) {
+        const GemmArgs gi = item(i);
         int rc;
         switch (algo) {
             case QG_ALGO_MFMA:
-                if (!mfma_eligible(gi)) return QG_ERR_UNSUPPORTED;
                 rc = hip_status(launch_mfma(gi, st));
                 break;
             case QG_ALGO_GENERIC:
@@ -373,6 +402,28 @@ int qg_debug_sumi(const void* A, const void* B, int32_t* sumi, int M, int N, int
     GemmArgs g;
     g.A = A; g.B = B; g.sumi = sumi; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
     g.ldc_m = N; g.ldc_n = 1;
+    return run_gemm(g, algo, (hipStream_t)stream);
+}
+
+int qg_debug_config(int M, int N, int K, int wtype, int algo, int sumi, char* buf, size_t len) {
+    if (!buf || len == 0) return QG_ERR_INVALID_ARG;
+    buf[0] = 0;
+    // 256-B aligned stand-in pointers: the shape decides, as for a real call on aligned buffers
+    GemmArgs g;
+    g.A = (const void*)256; g.B = (const void*)256; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    if (sumi) g.sumi = (int32_t*)256;
+    else g.C = (float*)256;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.describe = buf; g.describe_len = len;
+    return run_gemm(g, algo, nullptr);
+}
+
+int qg_gemm_w4a8_ldc(const void* A, const void* B, float* C, int M, int N, int K, int64_t ldc, int wtype, int algo,
+                     qg_stream_t stream) {
+    if (ldc < N || (M > 1 && ldc <= 0)) return QG_ERR_INVALID_ARG;
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = (long)ldc; g.ldc_n = 1;
     return run_gemm(g, algo, (hipStream_t)stream);
 }
 

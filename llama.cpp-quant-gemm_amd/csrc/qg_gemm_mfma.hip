@@ -23,8 +23,10 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
 // profiles/r01_tuning/mmq_probe_epi2.txt, mmq_probe_disp.txt, mmq_probe_lb.txt — M=8 5.56 -> 5.44
 // us, M=32 7.61 -> 7.39, M=64 10.35 -> 10.19, M=256 29.2 -> 27.1, M=512 58.3 -> 50.9, M=1024
 // 108.9 -> 96.5 (the 4-wave 32 x 32 tiles with the two-workgroups-per-CU register cap)
+// The sumi parity hook runs the same instantiation with SUMI = true (the EPI2 form's own operand
+// fragments and MFMAs; only the final accumulate becomes a store of each block's int32 dot).
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
-    if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16>(g, st);
+    if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true>(g, st);
     return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true>(g, st);
 }
 

@@ -20,7 +20,7 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     // (a strided batch uses the same shape, so its outputs equal the single launches' bit for bit;
     // the fused-quantization prologue is repeated per workgroup, so it keeps 16 rows per workgroup,
     // with the same per-row summation order)
-    if constexpr (MT <= 4 && !SUMI) {
+    if constexpr (MT <= 4) {
         if (nb % 2 == 0 && nb / 2 >= 64) {
             if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
                 return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
@@ -36,18 +36,21 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     return gemv_launch<F, MT, 2, 8, 256, SUMI, AIN>(g, st);
 }
 
-template <int F, int AIN> hipError_t launch_m(const GemmArgs& g, hipStream_t st) {
-    if (g.M <= 1) return launch_staged<F, 1, false, AIN>(g, st);
-    if (g.M <= 2) return launch_staged<F, 2, false, AIN>(g, st);
-    if (g.M <= 4) return launch_staged<F, 4, false, AIN>(g, st);
-    return launch_staged<F, 8, false, AIN>(g, st);
+// The sumi parity hook (SUMI = true) runs the very instantiation the product dispatch picks for
+// this shape — same MT, unit size, lanes per row, workgroup size, PRE and loop-free form — and only
+// replaces the final accumulate by a store of each block's int32 dot.
+template <int F, bool SUMI, int AIN> hipError_t launch_m(const GemmArgs& g, hipStream_t st) {
+    if (g.M <= 1) return launch_staged<F, 1, SUMI, AIN>(g, st);
+    if (g.M <= 2) return launch_staged<F, 2, SUMI, AIN>(g, st);
+    if (g.M <= 4) return launch_staged<F, 4, SUMI, AIN>(g, st);
+    return launch_staged<F, 8, SUMI, AIN>(g, st);
 }
 
 template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
-    if (g.sumi) return launch_staged<F, 8, true, AIN_Q8_1>(g, st);
-    if (g.ain == AIN_F32) return launch_m<F, AIN_F32>(g, st);
-    if (g.ain == AIN_F16_FUSED) return launch_m<F, AIN_F16_FUSED>(g, st);
-    return launch_m<F, AIN_Q8_1>(g, st);
+    if (g.sumi) return launch_m<F, true, AIN_Q8_1>(g, st);
+    if (g.ain == AIN_F32) return launch_m<F, false, AIN_F32>(g, st);
+    if (g.ain == AIN_F16_FUSED) return launch_m<F, false, AIN_F16_FUSED>(g, st);
+    return launch_m<F, false, AIN_Q8_1>(g, st);
 }
 
 template <int F> bool ok_f(const GemmArgs& g) {

@@ -392,6 +392,11 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
     const bool one = g.K / QK / BPL <= LPR;
+    if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
+        describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d grid=%dx%d", F, MT, BPL,
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (int)one, grid, g.batch);
+        return hipSuccess;
+    }
     // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4)
     auto kfn = one ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
                    : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE && (MT <= 2), false>;

@@ -85,6 +85,10 @@ __global__ __launch_bounds__(256) void generic_kernel(const uint8_t* __restrict_
 namespace {
 template <int F> hipError_t launch_g(const GemmArgs& g, hipStream_t st) {
     dim3 grid((g.N + 3) / 4, g.M);
+    if (g.describe) {
+        describe_kernel(g, "generic F=%d grid=%ux%u", F, grid.x, grid.y);
+        return hipSuccess;
+    }
     if (g.sumi)
         hipLaunchKernelGGL((generic_kernel<F, true>), grid, dim3(256), 0, st, (const uint8_t*)g.A,
                            (const uint8_t*)g.B, g.C, g.sumi, g.M, g.N, g.K, g.ldc_m, g.ldc_n);

@@ -23,13 +23,21 @@ struct GemmArgs {
     long sA = 0, sB = 0, sC = 0; // batch strides: bytes, bytes, floats
     void* ws = nullptr;          // optional device workspace (split-K partials + tile counters)
     size_t ws_bytes = 0;
+    char* describe = nullptr;    // qg_debug_config: the leaf launcher writes the kernel it would
+    size_t describe_len = 0;     // launch here (family + template parameters) and launches nothing
 };
 
-// GEMV / small batch (M <= 8), register-resident super-block decode + v_dot4.
+// printf-style description of a kernel instantiation into g.describe (qg_debug_config). SUMI is
+// deliberately not part of it: the parity hook must name the product's kernel.
+void describe_kernel(const GemmArgs& g, const char* fmt, ...);
+
+// GEMV / small batch (M <= 8): nibble-plane v_dot8 (Q4_0 / Q4_1) or v_dot4 (Q5_x / Q8_0) on
+// register-resident weight units, activation records staged in LDS.
 bool gemv_eligible(const GemmArgs& g);
 hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
 
-// Prefill (M > 8): LDS-staged activations, v_mfma_i32_32x32x32_i8 per Q-block.
+// Prefill (M >= 5): LDS-DMA staged weights + activations, one v_mfma_i32_16x16x32_i8 per Q-block,
+// MFMA-assisted (v_mfma_f32_16x16x16_f16) scale epilogue.
 bool mfma_eligible(const GemmArgs& g);
 hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
 

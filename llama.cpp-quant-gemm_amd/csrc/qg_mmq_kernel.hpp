@@ -171,14 +171,18 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     MMQ_STAMP(0);
 
     // per-lane DMA source offsets within a stage (rows / tokens past the edge read the last valid
-    // one; their results are dropped)
-    auto wpiece = [&](int p) {  // weight piece p of a stage: byte offset in B
+    // one; their results are dropped), relative to the workgroup's first row / token: the 64-bit
+    // bases Bw / Aw carry n0 * RB and m0 * AB, so tensors beyond 2 GiB address correctly and the
+    // per-lane offsets stay below BN * RB (mmq_shape_ok)
+    const uint8_t* Bw = B + (long)n0 * RB;
+    const uint8_t* Aw = A + (long)m0 * AB;
+    auto wpiece = [&](int p) {  // weight piece p of a stage: byte offset from Bw
         const int row = p / G::PPR;
-        return (int)((long)min(n0 + row, N - 1) * RB) + (p - row * G::PPR) * G::WPS;
+        return (min(n0 + row, N - 1) - n0) * (int)RB + (p - row * G::PPR) * G::WPS;
     };
-    auto apiece = [&](int p) {  // activation piece p of a stage: byte offset in A
+    auto apiece = [&](int p) {  // activation piece p of a stage: byte offset from Aw
         const int tok = p / G::APT;
-        return (int)((long)min(m0 + tok, M - 1) * AB) + min(p - tok * G::APT, G::APR - 1) * 16;
+        return (min(m0 + tok, M - 1) - m0) * (int)AB + min(p - tok * G::APT, G::APR - 1) * 16;
     };
     constexpr int NOFF = G::CMB ? G::NI : 1;
     int woff[G::CMB ? 1 : G::NWI], aoff[G::CMB ? 1 : G::NAI], coff[NOFF];
@@ -203,8 +207,8 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     // per-lane M0 base, read back with v_readfirstlane — wrong destinations for half the wave
     // (found by tools/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
-        const uint8_t* wsrc = B + (long)h * G::RSB - G::shift(h);
-        const uint8_t* asrc = A + (long)h * (SB * Q8_1_BYTES);
+        const uint8_t* wsrc = Bw + (long)h * G::RSB - G::shift(h);
+        const uint8_t* asrc = Aw + (long)h * (SB * Q8_1_BYTES);
         if constexpr (G::CMB) {
 #pragma unroll
             for (int i = 0; i < G::NI; ++i) glds<16>((cisw[i] ? wsrc : asrc) + coff[i], buf + 64 * i * 16);
@@ -220,6 +224,43 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
     for (int i = 0; i < G::NACC; ++i) acc[i] = 0.0f;
     const v4i bias = {MMQ_BIAS, MMQ_BIAS, MMQ_BIAS, MMQ_BIAS};
+
+    // Operand fragments of one block, shared by both epilogue forms (so the parity hook's sumi, which
+    // runs the product's EPI2 form, covers exactly the product's decode): the weight row's k-slot q
+    // (elements 4q..4q+3 | 16+4q..16+4q+3 as low / high nibbles, + qh bits for Q5_x, or Q8_0's
+    // signed qs dwords q and 4+q), and the token's qs dwords q and 4+q.
+    auto wfrag = [&](const uint8_t* wr, auto O) -> long {
+        constexpr int o = decltype(O)::value;  // block's byte offset in the row image
+        uint32_t lo, hi;
+        if constexpr (T::Q8) {
+            lo = lds32<o + T::QS>(wr + 4 * q);
+            hi = lds32<o + T::QS + 16>(wr + 4 * q);
+        } else {
+            const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
+            lo = v & 0x0F0F0F0Fu;
+            hi = (v >> 4) & 0x0F0F0F0Fu;
+        }
+        if constexpr (T::QH >= 0) {
+            const uint32_t qh = lds32<o + T::QH>(wr);
+            lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
+            hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
+        }
+        return (long)(((unsigned long)hi << 32) | lo);
+    };
+    auto afrag_of = [&](const uint8_t* ar) -> long {
+        const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
+        const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
+        return (long)(((unsigned long)qa1 << 32) | qa0);
+    };
+    // sumi parity hook: the block's int32 dots of this lane's 4 rows x its token
+    auto store_sumi = [&](const v4i& c, int i, int t, int h, int b) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int n = n0 + 16 * i + 4 * q + e, m = m0 + 16 * t + r16;
+            if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * SB + b] = c[e] - MMQ_BIAS;
+        }
+    };
+
 
     // Block scales straight from the staged images, per lane: the f16 bits of d_w (and m_w) of the
     // 4 weight rows 16 i + 4 q + e it accumulates (used as f16 by v_fma_mix_f32, no convert), and
@@ -244,11 +285,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 if constexpr (SUMI) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int n = n0 + 16 * i + 4 * q + e, m = m0 + 16 * t + r16;
-                        if (n < N && m < M) sumi_out[((long)m * N + n) * nb + h * SB + b] = p.c[i][t][e] - MMQ_BIAS;
-                    }
+                    store_sumi(p.c[i][t], i, t, h, b);
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; e += 2) {
@@ -302,6 +339,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     auto h4 = [](unsigned long v) { return __builtin_bit_cast(f16x4, v); };
     auto compute4_e2 = [&](uint8_t* buf, int h, int sh, auto SUB) {
         constexpr int b0 = 4 * decltype(SUB)::value;
+        (void)h;
         long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
         uint32_t wdb[MMQ_SB][G::RT], wmb[MMQ_SB][G::RT], adb[MMQ_SB][TT];
         const bool q0 = q == 0;
@@ -311,30 +349,14 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
-                uint32_t lo, hi;
-                if constexpr (T::Q8) {
-                    lo = lds32<o + T::QS>(wr + 4 * q);
-                    hi = lds32<o + T::QS + 16>(wr + 4 * q);
-                } else {
-                    const uint32_t v = lds32<o + T::QS>(wr + 4 * q);
-                    lo = v & 0x0F0F0F0Fu;
-                    hi = (v >> 4) & 0x0F0F0F0Fu;
-                }
-                if constexpr (T::QH >= 0) {
-                    const uint32_t qh = lds32<o + T::QH>(wr);
-                    lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
-                    hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
-                }
-                afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
+                afrag[b][i] = wfrag(wr, ic<o>{});
                 wdb[b][i] = u16(wr + o);
                 if constexpr (HAS_M) wmb[b][i] = u16(wr + o + T::MOFF);
             }
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * G::ASTR + (b0 + b) * Q8_1_BYTES;
-                const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
-                const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
-                bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
+                bfrag[b][t] = afrag_of(ar);
                 adb[b][t] = *reinterpret_cast<const uint32_t*>(ar);  // f16 d_a | f16 s_a << 16
             }
         });
@@ -387,6 +409,16 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SUMI) {
+            static_for<MMQ_SB>([&](auto BI) {
+                constexpr int b = decltype(BI)::value;
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) store_sumi(cc[b][i][t], i, t, h, b0 + b);
+            });
+            return;
+        }
         static_for<MMQ_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
 #pragma unroll
@@ -405,7 +437,6 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
                     }
         });
         __builtin_amdgcn_sched_barrier(0);
-        (void)h;
     };
 
     auto compute4 = [&](uint8_t* buf, int h, int sh, auto SUB) {
@@ -418,21 +449,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
-                uint32_t lo, hi;
-                if constexpr (T::Q8) {  // signed bytes, elements 4q.. and 16+4q..
-                    lo = lds32<o + T::QS>(wr + 4 * q);
-                    hi = lds32<o + T::QS + 16>(wr + 4 * q);
-                } else {
-                    const uint32_t v = lds32<o + T::QS>(wr + 4 * q);  // 4q keeps the alignment
-                    lo = v & 0x0F0F0F0Fu;
-                    hi = (v >> 4) & 0x0F0F0F0Fu;
-                }
-                if constexpr (T::QH >= 0) {
-                    const uint32_t qh = lds32<o + T::QH>(wr);
-                    lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
-                    hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
-                }
-                afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
+                afrag[b][i] = wfrag(wr, ic<o>{});
                 const uint8_t* sr = buf + (16 * i + 4 * q) * G::RIMG + sh + o;  // rows 16 i + 4 q + e
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -443,9 +460,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * G::ASTR + (b0 + b) * Q8_1_BYTES;
-                const uint32_t qa0 = *reinterpret_cast<const uint32_t*>(ar + 4 + 4 * q);
-                const uint32_t qa1 = *reinterpret_cast<const uint32_t*>(ar + 20 + 4 * q);
-                bfrag[b][t] = (long)(((unsigned long)qa1 << 32) | qa0);
+                bfrag[b][t] = afrag_of(ar);
                 const uint32_t dsh = *reinterpret_cast<const uint32_t*>(ar);
                 const float da = h2f(dsh & 0xFFFFu), sa = h2f(dsh >> 16);
                 const float nda = -(da * MMQ_BIAS_F), ncs = -(CS * sa);
@@ -480,7 +495,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     };
 
     auto compute = [&](uint8_t* buf, int h, int sh) {
-        if constexpr (EPI2 && !SUMI && ABL == 0)
+        if constexpr (EPI2 && ABL == 0)
             static_for<SB / 4>([&](auto SUB) { compute4_e2(buf, h, sh, SUB); });
         else
             static_for<SB / 4>([&](auto SUB) { compute4(buf, h, sh, SUB); });
@@ -583,7 +598,8 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 }
 
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
-// rows and stages aligned to the DMA piece, 32-bit byte offsets. P16 additionally: a 16-B aligned B
+// rows and stages aligned to the DMA piece, one workgroup's rows / tokens within 2 GiB (tensors of
+// any size otherwise). P16 additionally: a 16-B aligned B
 // and rows, and K % 256 == 0 when a stage segment is not a 16-B multiple (see mmq_geom).
 // Workspace of a split-K (KS > 1) launch: one counter per output tile (zero before the first
 // launch; every launch leaves them zero), then KS partial tiles per output tile.
@@ -603,7 +619,8 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     if (((uintptr_t)g.A & 15) != 0 || AB % 16 != 0) return false;
     if (P16 && G::RSB % 16 != 0 && g.K % 256 != 0) return false;
     if (((uintptr_t)g.B % G::WPS) != 0 || RB % G::WPS != 0) return false;
-    if (RB * g.N >= (1L << 31) || AB * g.M >= (1L << 31)) return false;
+    // per-lane DMA offsets are 32-bit relative to the workgroup's 64-bit row / token base
+    if (RB * BN >= (1L << 31) || AB * G::NTOK >= (1L << 31)) return false;
     return true;
 }
 
@@ -613,6 +630,11 @@ hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK, KS);
     auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2>;
+    if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
+        describe_kernel(g, "mmq F=%d BN=%d TT=%d W=%d P16=%d NB=%d ABL=%d ROT=%d SB=%d KS=%d EPI2=%d grid=%ux%ux%u", F, BN,
+                        TT, W, (int)P16, NB, ABL, (int)ROT, SB, KS, (int)EPI2, grid.x, grid.y, grid.z);
+        return hipSuccess;
+    }
     unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;
     float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
     if (G::LDS > 64 * 1024) {

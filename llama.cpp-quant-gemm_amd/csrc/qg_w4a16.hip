@@ -666,6 +666,12 @@ struct w16_plan {
     long gx = 0, gy = 0;
     size_t ws_bytes = 0;  // workspace for ks > 1: tile counters, then ks partial tiles per tile
 };
+// Workspace layout, the same for every shape: W16_CNT_BYTES of tile counters (split-K runs only
+// while the grid has < 512 tiles), then the partial tiles. A fixed counter region keeps the
+// counters zero across shapes: every launch re-arms its own counters, and no other shape's
+// partial tiles ever overlap them (a shape-dependent offset let one shape's partials
+// land in another shape's counters on a shared workspace).
+constexpr size_t W16_CNT_BYTES = 4096;
 
 w16_plan w16_make_plan(int M, int N, int K) {
     w16_plan p;
@@ -688,8 +694,8 @@ w16_plan w16_make_plan(int M, int N, int K) {
             p.ks = d;
             if (p.gx * p.gy * d >= want) break;
         }
-    if (p.ks > 1)
-        p.ws_bytes = ((size_t)p.gx * p.gy * 4 + 255) / 256 * 256 + (size_t)p.gx * p.gy * p.ks * p.rt * p.tt * 4 * 64 * 4;
+    static_assert(W16_CNT_BYTES / 4 >= 512, "counter region holds every split-K grid");
+    if (p.ks > 1) p.ws_bytes = W16_CNT_BYTES + (size_t)p.gx * p.gy * p.ks * p.rt * p.tt * 4 * 64 * 4;
     return p;
 }
 
@@ -697,7 +703,7 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
                                                                   hipStream_t st) {
     const int ks = ws ? p.ks : 1;
     unsigned* cnt = (unsigned*)ws;
-    float* part = ws ? (float*)((uint8_t*)ws + ((size_t)p.gx * p.gy * 4 + 255) / 256 * 256) : nullptr;
+    float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
     constexpr size_t lds = (size_t)TT * KB * 3 * 1024;
     auto kfn = w16_sk_kernel<F, RT, TT, KB>;
     if (lds > 64 * 1024) {

@@ -115,7 +115,11 @@ def _check_blocks(t: torch.Tensor, what: str, rows: int, K: int, bb: int) -> Non
 def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
               wtype: int = Q4_0, algo: int = ALGO_AUTO, out: torch.Tensor | None = None) -> torch.Tensor:
     """Activation-major C[M, N] = A_q8_1[M, K] . B_w[N, K]^T (include/gemm_reference.h:175-222;
-    include/llama_adapter.h). M = tokens, N = weight rows."""
+    include/llama_adapter.h). M = tokens, N = weight rows.
+
+    ``out``: optional float32 [M, N] destination; its rows may be strided (``out.stride(1) == 1``,
+    ``out.stride(0) >= N``, e.g. a column slice of a wider buffer), written through
+    ``qg_gemm_w4a8_ldc``."""
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
     _require(wtype in WEIGHT_TYPES, f"unsupported weight type {wtype}")
     _check_blocks(activation_q, "Activation", M, K, 36)
@@ -125,10 +129,14 @@ def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=w.device)
     else:
-        _require(out.is_contiguous() and out.dtype == torch.float32 and out.numel() == M * N, "bad out tensor")
+        _require(out.is_cuda and out.dtype == torch.float32 and tuple(out.shape) == (M, N), "bad out tensor")
+        _require(out.device == w.device, "out must be on the weights' device")
+        _require(M * N == 0 or out.stride(1) == 1 or N == 1, "bad out tensor: rows must be dense")
+    ldc = out.stride(0) if M > 1 else N
+    _require(ldc >= N, "bad out tensor: row stride below N")
     with torch.cuda.device(w.device):
-        _lib.check(_lib.load().qg_gemm_w4a8_ex(_ptr(a), _ptr(w), _ptr(out), M, N, K, wtype, algo,
-                                               _stream(w.device)), "gemm_w4a8")
+        _lib.check(_lib.load().qg_gemm_w4a8_ldc(_ptr(a), _ptr(w), _ptr(out), M, N, K, ldc, wtype, algo,
+                                                _stream(w.device)), "gemm_w4a8")
     return out
 
 
@@ -305,6 +313,14 @@ def debug_sumi(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: in
     return out
 
 
+def debug_config(M: int, N: int, K: int, wtype: int = Q4_0, algo: int = ALGO_AUTO, sumi: bool = False) -> str:
+    """The kernel instantiation ``gemm_w4a8`` (or ``debug_sumi`` with sumi=True) launches for this
+    shape on aligned buffers (family, template parameters, grid); nothing is launched."""
+    buf = ctypes.create_string_buffer(256)
+    _lib.check(_lib.load().qg_debug_config(M, N, K, wtype, algo, int(sumi), buf, 256), "debug_config")
+    return buf.value.decode()
+
+
 def select_algo(M: int, N: int, K: int, wtype: int = Q4_0) -> int:
     return _lib.load().qg_select_algo(M, N, K, wtype)
 
@@ -319,7 +335,7 @@ __all__ = [
     "quantize_q4_0", "quantize_q8_1", "gemm_q4_0_q8_1", "dequantize_q4_0",
     "QK4_0", "QK8_1", "BLOCK_Q4_0_BYTES", "BLOCK_Q8_1_BYTES",
     "quantize", "dequantize", "gemm_w4a8", "gemm_q4_1_q8_1", "gemm_q5_0_q8_1", "gemm_q5_1_q8_1",
-    "gemm_w4a8_batched", "debug_sumi", "select_algo", "version",
+    "gemm_w4a8_batched", "debug_sumi", "debug_config", "select_algo", "version",
     "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused", "gemm_w8a8", "gemm_q8_0_q8_1",
     "gemm_w4a16", "gemm_w8a16", "gemm_q4_0_fp32",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",

@@ -65,12 +65,17 @@ class RowShardedW4A8:
         return torch.empty((self.world, M, self.rows), dtype=torch.float32, device=self.weight.device)
 
     def compute_local(self, act_q: torch.Tensor, M: int, out: torch.Tensor) -> torch.Tensor:
+        """out[M, rows]: this rank's slice. A ragged last shard (local < rows) writes the column
+        view out[:, :local] — rows strided by ``rows`` floats, which the HIP entry point takes as
+        its output row stride (qg_gemm_w4a8_ldc); the padding columns keep their contents."""
         local = self.stop - self.start
         if local > 0:
             self.compute(act_q, self.weight, M, local, self.K, out[:, :local] if local < self.rows else out)
         return out
 
     def gather(self, out: torch.Tensor, gathered: torch.Tensor, async_op: bool = False):
+        """One all-gather of every rank's ``out`` (any leading dims, e.g. [G, M, rows] for G
+        independent products) into ``gathered`` [world, *out.shape]."""
         if self.world == 1:
             gathered[0].copy_(out)
             return None

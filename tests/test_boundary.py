@@ -72,8 +72,9 @@ def test_static_queries(lib):
     assert so.qg_select_algo(1, 4096, 33, 2) == -1
     assert so.qg_status_string(-2).decode().startswith("K must be")
     # W4A16 prefill split-K workspace (host-side plan): 512 workgroups of 64 rows x 32 tokens x
-    # K/8 at M=32, N=K=4096 -> 64 tiles x 8 slices x 8 KB of partials + the tile counters
-    assert so.qg_gemm_w16_workspace_size(32, 4096, 4096) == 256 + 64 * 8 * 4 * 2 * 4 * 64 * 4
+    # K/8 at M=32, N=K=4096 -> the fixed 4 KB tile-counter region + 64 tiles x 8 slices x 8 KB of
+    # partials (the counter region does not move with the shape: ADVICE r01)
+    assert so.qg_gemm_w16_workspace_size(32, 4096, 4096) == 4096 + 64 * 8 * 4 * 2 * 4 * 64 * 4
     assert so.qg_gemm_w16_workspace_size(4, 4096, 4096) == 0      # GEMV: no workspace
     assert so.qg_gemm_w16_workspace_size(512, 4096, 4096) == 0    # enough token tiles: no split
 
@@ -156,3 +157,40 @@ def test_python_mirror_errors_match_reference():
         q.gemm_q4_0_q8_1(torch.zeros(4, 2, 18, dtype=torch.uint8), torch.zeros(1, 2, 36, dtype=torch.uint8), 4, 1, 64)
     with pytest.raises(RuntimeError, match="K must be divisible by 32"):
         q.gemm_q4_0_q8_1(torch.zeros(1, dtype=torch.uint8), torch.zeros(1, dtype=torch.uint8), 4, 1, 65)
+
+
+# The sumi parity hook must run the product's own kernel instantiation: the
+# configuration query names the kernel qg_gemm_w4a8_ex and qg_debug_sumi would launch.
+PRODUCT_SHAPES = [(1, 4096, 4096), (2, 4096, 4096), (3, 4096, 4096), (4, 4096, 4096), (8, 4096, 4096),
+                  (32, 4096, 4096), (1, 4000, 4096), (1, 32000, 4096), (5, 4096, 4096), (128, 4096, 4096),
+                  (512, 4096, 4096), (1, 4096, 14336), (3, 11008, 4096)]
+
+
+@pytest.mark.parametrize("m,n,k", PRODUCT_SHAPES)
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+def test_sumi_hook_runs_product_kernel(lib, m, n, k, t):
+    import quant_gemm as qg
+    prod = qg.debug_config(m, n, k, t)
+    assert prod and prod == qg.debug_config(m, n, k, t, sumi=True)
+    fam = {1: "gemv", 2: "mmq", 3: "generic"}[qg.select_algo(m, n, k, t)]
+    assert prod.startswith(fam + " ")
+
+
+def test_headline_configs_kernels(lib):
+    """The kernels serving BASELINE configs[1..4] (what DESIGN.md §3 documents)."""
+    import quant_gemm as qg
+    assert qg.debug_config(1, 4096, 4096, 2).startswith("gemv F=2 MT=1 BPL=2 LPR=64 WGS=1024")
+    assert "ONEU=1" in qg.debug_config(1, 4096, 4096, 2)
+    assert qg.debug_config(32, 4096, 4096, 2).startswith("mmq F=2 ")
+    assert "EPI2=1" in qg.debug_config(32, 4096, 4096, 2)
+    for t in (3, 6, 7):
+        assert qg.debug_config(1, 4096, 4096, t).startswith(f"gemv F={t} MT=1 ")
+    assert qg.debug_config(1, 4000, 4096, 2).startswith("gemv F=2 MT=1 ")
+
+
+def test_ldc_entry_validates(lib):
+    so = lib.load()
+    P = ctypes.c_void_p
+    # ldc below N is an invalid argument, reported before anything is enqueued
+    assert so.qg_gemm_w4a8_ldc(P(256), P(256), P(256), 2, 64, 256, 32, 2, 0, None) == -1
+    assert so.qg_gemm_w4a8_ldc(P(256), P(256), P(256), 2, 64, 100, 64, 2, 0, None) == -2

@@ -2,7 +2,8 @@
 
 Bars:
   * quantizer / dequantizer bytes: bit-exact;
-  * per-block int32 sumi: bit-exact, through the SAME decode path each kernel family uses;
+  * per-block int32 sumi: bit-exact, computed by the very kernel instantiation the product
+    dispatch launches for the shape (qg_debug_config asserts the match; test_gpu_product.py);
   * fp32 outputs: per-block terms are computed in the reference's operation order without
     contraction, so the only admissible difference is fp32 summation order:
     |C_gpu - C_ref| <= 2 * nb * 2^-24 * sum_b |term_b|   (oracle.summation_tol);
@@ -327,13 +328,18 @@ def test_baseline_q4_0_full_size(O, qg, m, n, k, bound):
     assert abs(O.nmse(c, c_fp32) - O.nmse(c_ref, c_fp32)) < 1e-9
 
 
-@pytest.mark.parametrize("t,bound", [(2, 5e-3), (3, 4.5e-3), (6, 1.5e-3), (7, 1.2e-3)])
+# bounds just above the oracle's NMSE on this recipe (4.5550e-3, 3.7749e-3, 1.0032e-3, 8.7440e-4 with
+# the include/quantize.h Q8_1 quantizer; the reference-compiled values with the test_framework one,
+# tests/golden/kat.json, are asserted on the oracle in tests/test_oracle.py)
+@pytest.mark.parametrize("t,bound", [(2, 4.56e-3), (3, 3.78e-3), (6, 1.005e-3), (7, 8.75e-4)])
 def test_allquants_full_size(O, qg, t, bound):
     """BASELINE configs[3]: Q4_1/Q5_0/Q5_1 (and Q4_0) x Q8_1 GEMV at M=1, N=K=4096."""
     a, b, aq, bq = make_case(O, 1, 4096, 4096, t)
     c = host(qg.gemm_w4a8(dev(aq), dev(bq), 1, 4096, 4096, t))
-    assert_close_to_oracle(O, c, aq, bq, t)
-    assert O.nmse(c, O.gemm_fp32(a, b)) <= bound
+    c_ref = assert_close_to_oracle(O, c, aq, bq, t)
+    c_fp32 = O.gemm_fp32(a, b)
+    assert O.nmse(c, c_fp32) <= bound
+    assert abs(O.nmse(c, c_fp32) - O.nmse(c_ref, c_fp32)) <= 1e-6 * bound
 
 
 # ------------------------------------------------------------------------------- full-size properties

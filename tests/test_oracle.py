@@ -243,3 +243,26 @@ def test_w8a16_oracle_vs_fp64(O):
     c = O.gemm_w8a16(a, bq)
     exact = a.astype(np.float64) @ O.dequantize(bq, O.Q8_0).astype(np.float64).T
     assert (np.abs(c - exact) <= O.w16_tol(a, bq, O.Q8_0)).all()
+
+
+# NMSE vs FP32 recorded in SURVEY.md Appendix A from the reference compiled in the survey container
+# (gemm_w4a8_reference / gemm_fp32_reference; the all-quants row with the test_framework quantizers,
+# tests/framework/test_framework.cuh:195-367, i.e. Q8_1 variant 1). Five significant figures of
+# NMSE over 4096 outputs fingerprint the quantizer and dot restatements, incl. the Q4_1/Q5_0/Q5_1
+# ones no reference-held byte vector pins.
+@pytest.mark.parametrize("key,m,n,k", [("m1_n128_k256", 1, 128, 256), ("m1_n4096_k4096", 1, 4096, 4096),
+                                       ("m32_n4096_k4096", 32, 4096, 4096), ("m1_n32000_k4096", 1, 32000, 4096)])
+def test_recorded_nmse_q4_0(O, key, m, n, k):
+    a, b = O.fill_uniform_step4(m, n, k, 42)
+    c = O.gemm_w4a8(O.quantize(a, O.Q8_1), O.quantize(b, O.Q4_0))
+    want = KAT["nmse_vs_fp32"][key]
+    assert abs(O.nmse(c, O.gemm_fp32(a, b)) - want) <= 5e-5 * want
+
+
+@pytest.mark.parametrize("name,t", [("q4_0", 2), ("q4_1", 3), ("q5_0", 6), ("q5_1", 7)])
+def test_recorded_nmse_allquants(O, name, t):
+    a, b = O.fill_uniform_step4(1, 4096, 4096, 42)
+    c = O.gemm_w4a8(O.quantize(a, O.Q8_1, 1), O.quantize(b, t), t)
+    want = KAT["nmse_vs_fp32"]["allquants_m1_n4096_k4096"][name]
+    # printed with 5 significant figures; the FP32 reference's float summation may move the last
+    assert abs(O.nmse(c, O.gemm_fp32(a, b)) - want) <= 1.5e-4 * want
