@@ -216,11 +216,15 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // ONEU: every lane owns at most one unit (K <= 32 * BPL * LPR): the kernel has no unit loop, so the
 // waits for the weight loads sit at their first use, behind the record reads (with a loop in the
 // kernel, hipcc's wait insertion falls back to vmcnt(0) before the first record read).
+// Argument order: everything the first loads need (A, B, their batch strides, M, N, K) sits in the
+// first 14 dwords, which the dispatch preloads into SGPRs (-amdgpu-kernarg-preload-count, Makefile);
+// the rest (output pointer and strides, the sumi hook) is fetched by an s_load that is only waited
+// for at the store, so no kernarg fetch sits in front of the weight stream.
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
           bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                   float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
-                                                   int N, int K, long ldc_m, long ldc_n, long sA, long sB, long sC) {
+                                                   long sA, long sB, int M, int N, int K, float* __restrict__ C,
+                                                   long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
     using G = gemv_geom<F, BPL>;
     QG_STAMP(t0);
     QG_CLK(c0);
@@ -404,8 +408,8 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kfn, dim3(grid, g.batch), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.C,
-                       g.sumi, g.M, g.N, g.K, g.ldc_m, g.ldc_n, g.sA, g.sB, g.sC);
+    hipLaunchKernelGGL(kfn, dim3(grid, g.batch), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.sA,
+                       g.sB, g.M, g.N, g.K, g.C, g.sC, g.ldc_m, g.ldc_n, g.sumi);
     return hipGetLastError();
 }
 

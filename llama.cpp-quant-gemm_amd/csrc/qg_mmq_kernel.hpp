@@ -28,9 +28,13 @@
 // in fixed wave order through LDS at the end.
 //
 // A stage runs in three phases (all LDS reads, all MFMAs, all epilogues) so that each phase's
-// latencies overlap; MFMA results are read behind an explicit wait: reading them with only the wait
-// states hipcc inserts for this instruction on gfx950 gave wrong sums (tools/mmq_debug.hip). Only
-// LDS reads in the main loop: an LDS write there makes hipcc wait for every DMA in flight.
+// latencies overlap. MFMA results -> VALU: gfx950 needs 8 wait states after v_mfma_i32_16x16x32_i8
+// and v_mfma_f32_16x16x16_f16 (tools/mfma_hazard_probe.hip on an MI355X: every lane wrong at <= 6
+// states, right from 8; profiles/r02_tuning/mfma_hazard_probe.txt) and hipcc pads exactly 8
+// (`s_nop 7`); tests/test_isa_hazards.py checks every MFMA of the shipped code object for it. The
+// `s_nop 7; s_nop 7` after each MFMA phase below is a margin on top (the round-1 wrong sums that
+// first prompted it came from an MFMA result element read through a bit_cast, mmq_probe1-2.txt).
+// Only LDS reads in the main loop: an LDS write there makes hipcc wait for every DMA in flight.
 #pragma once
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
@@ -92,7 +96,14 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // SB: blocks per stage (4 or 8). With 8, every format's stage segment is a 16-B multiple (no
 // shifted windows) and each token's activation segment is 288 B (+16 B pad against 2-way LDS bank
 // conflicts).
-template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4> struct mmq_geom {
+// OPT bit flags (tuning; see mmq_opt below): MMQ_CONTIG — each wave owns a contiguous range of
+// K stages (its consecutive stages are adjacent bytes of every row, fetched back to back), instead
+// of stages w, w + W, ...; MMQ_ZL — lanes that must feed zeros into the scale MFMAs (k-slots 1..15)
+// read their scales from a zeroed per-wave LDS region instead of selecting zeros in VALU.
+enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2 };
+constexpr int MMQ_ZB = 1024;  // bytes of the per-wave zero region (covers every scale offset)
+
+template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4, int OPT = 0> struct mmq_geom {
     using T = wfmt<F>;
     static_assert(SB == 4 || SB == 8 || SB == 16, "4, 8 or 16 blocks per stage");
     static constexpr int RSB = SB * T::BB;                     // weight bytes per row per stage
@@ -116,7 +127,9 @@ template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4
     static constexpr int BUF = CMB ? NI * 64 * 16 : OFF_A + NAI * 64 * 16;
     static constexpr int NACC = RT * TT * 4;                   // accumulators per lane
     // wave buffers; the end-of-kernel partial tiles reuse them (after a barrier)
-    static constexpr size_t LDS = (size_t)W * (NB * BUF > NACC * 256 ? NB * BUF : NACC * 256);
+    static constexpr size_t LDS0 = (size_t)W * (NB * BUF > NACC * 256 ? NB * BUF : NACC * 256);
+    static constexpr size_t ZOFF = LDS0;                                   // per-wave zero regions
+    static constexpr size_t LDS = LDS0 + ((OPT & MMQ_ZL) ? (size_t)W * MMQ_ZB : 0);
     static_assert(NB >= 1 && NB <= 4, "1..4 stage buffers per wave");
     static_assert(LDS <= 160 * 1024, "LDS per workgroup");
     static_assert(OFF_A % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
@@ -141,15 +154,16 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // per output tile) sums the KS partials in slice order (deterministic: the same order whichever
 // workgroup arrives last) and re-arms the counter to 0 for the next launch.
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1, bool EPI2 = false>
+          int KS = 1, bool EPI2 = false, int OPT = 0>
 // (4-wave workgroups: at least two per CU, i.e. <= 256 VGPRs — without the cap the EPI2 form took
 // 320 and ran one workgroup per CU, 13 % slower at M=512 than with it)
 __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                      float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
                                                      int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
                                                      unsigned* __restrict__ cnt) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB, OPT>;
     using T = wfmt<F>;
+    constexpr bool ZL = (OPT & MMQ_ZL) != 0 && EPI2;
     static_assert(BN % 16 == 0 && BN <= 64 && TT >= 1 && TT <= 4, "row tiles of 16, <= 64 tokens");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -165,6 +179,11 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     const long RB = (long)nb * T::BB;
     const long AB = (long)nb * Q8_1_BYTES;
     uint8_t* bufs = smem + wave * NB * G::BUF;
+    uint8_t* zb = smem + G::ZOFF + (ZL ? wave * MMQ_ZB : 0);  // this wave's zero region (ZL)
+    if constexpr (ZL) {
+        static_assert(MMQ_ZB == 64 * 16, "one 16-B store per lane");
+        *reinterpret_cast<uint4*>(zb + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);  // read only by this wave
+    }
 #ifdef QG_MMQ_STAMPS
     unsigned long long stamps[8] = {};
 #endif
@@ -314,8 +333,8 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     // The 4 blocks of one staged stage in three phases, so each phase's latencies overlap: every
     // LDS read of the stage (operand fragments and block scales) in flight together, then the
     // 4 x RT x TT MFMAs back to back, then the VALU epilogues (block b's results are read behind
-    // the later blocks' MFMAs and epilogues, plus an explicit wait for the matrix pipe: reading
-    // them with only the wait states hipcc inserts gave wrong sums, tools/mmq_debug.hip).
+    // the later blocks' MFMAs and epilogues, plus a 16-state margin over the 8 the hardware needs:
+    // see the header).
     // EPI2 (!SUMI): the scale arithmetic moves onto the matrix pipe. Per block, one
     // v_mfma_f32_16x16x16_f16 forms the outer product d_w (x) d_a (k-slot 0 only: exact f16 x f16 in
     // f32) in the accumulator layout, so the VALU epilogue is sumi = cf - 1.5*2^23 (exact) and
@@ -350,14 +369,17 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
                 afrag[b][i] = wfrag(wr, ic<o>{});
-                wdb[b][i] = u16(wr + o);
-                if constexpr (HAS_M) wmb[b][i] = u16(wr + o + T::MOFF);
+                const uint8_t* ws = ZL ? (q0 ? wr : zb) : wr;  // ZL: lanes q > 0 read zeros
+                wdb[b][i] = u16(ws + o);
+                if constexpr (HAS_M) wmb[b][i] = u16(ws + o + T::MOFF);
             }
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                const uint8_t* ar = buf + G::OFF_A + (16 * t + r16) * G::ASTR + (b0 + b) * Q8_1_BYTES;
+                const uint8_t* a0 = buf + G::OFF_A + (16 * t + r16) * G::ASTR;
+                const uint8_t* ar = a0 + (b0 + b) * Q8_1_BYTES;
                 bfrag[b][t] = afrag_of(ar);
-                adb[b][t] = *reinterpret_cast<const uint32_t*>(ar);  // f16 d_a | f16 s_a << 16
+                const uint8_t* as = ZL ? (q0 ? a0 : zb) : a0;
+                adb[b][t] = *reinterpret_cast<const uint32_t*>(as + (b0 + b) * Q8_1_BYTES);  // f16 d_a | f16 s_a << 16
             }
         });
         __builtin_amdgcn_sched_barrier(0);
@@ -371,8 +393,9 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #pragma unroll
                 for (int t = 0; t < TT; ++t)
                     dd[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                        h4(q0 ? (unsigned long)(wdb[b][i] & 0xFFFFu) : 0ul),
-                        h4(q0 ? (unsigned long)(adb[b][t] & 0xFFFFu) : 0ul), z4, 0, 0, 0);
+                        h4(ZL ? (unsigned long)wdb[b][i] : q0 ? (unsigned long)(wdb[b][i] & 0xFFFFu) : 0ul),
+                        h4(ZL ? (unsigned long)(adb[b][t] & 0xFFFFu) : q0 ? (unsigned long)(adb[b][t] & 0xFFFFu) : 0ul),
+                        z4, 0, 0, 0);
         });
         static_for<MMQ_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
@@ -396,12 +419,12 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
                     x01 = __builtin_amdgcn_perm(wdb[1][i], wdb[0][i], 0x05040100u);
                     x23 = __builtin_amdgcn_perm(wdb[3][i], wdb[2][i], 0x05040100u);
                 }
-                const unsigned long xa = q0 ? (((unsigned long)x23 << 32) | x01) : 0ul;
+                const unsigned long xa = ZL || q0 ? (((unsigned long)x23 << 32) | x01) : 0ul;
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
                     const uint32_t s01 = __builtin_amdgcn_perm(adb[1][t], adb[0][t], 0x07060302u);
                     const uint32_t s23 = __builtin_amdgcn_perm(adb[3][t], adb[2][t], 0x07060302u);
-                    const unsigned long sb = q0 ? (((unsigned long)s23 << 32) | s01) : 0ul;
+                    const unsigned long sb = ZL || q0 ? (((unsigned long)s23 << 32) | s01) : 0ul;
                     c2[i][t] = __builtin_amdgcn_mfma_f32_16x16x16f16(h4(xa), h4(sb), c2[i][t], 0, 0, 0);
                 }
             }
@@ -505,9 +528,13 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     // of one XCD (blockIdx.x = c mod 8) start at different rounds of W stages, so they do not all
     // pull the same activation lines through their L2 at the same moment; each wave keeps its set
     // of stages (rotation by a multiple of W when W divides H), only their order changes.
-    const int nst = wave < H ? (H - 1 - wave) / W + 1 : 0;
+    // MMQ_CONTIG (H % W == 0): wave w owns stages w * H / W .. (w + 1) * H / W - 1 instead.
+    constexpr bool CONTIG = (OPT & MMQ_CONTIG) != 0;
+    const bool contig = CONTIG && H % W == 0;
+    const int nst = contig ? H / W : wave < H ? (H - 1 - wave) / W + 1 : 0;
     const int rot = ROT && H % W == 0 ? (int)(((blockIdx.x >> 3) * W) % H) : 0;
     auto stage = [&](int k) {
+        if (contig) return h0 + wave * nst + k;
         const int h = wave + rot + k * W;
         return h0 + (h >= H ? h - H : h);
     };
@@ -530,7 +557,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
     MMQ_STAMP(3);
 
     if constexpr (EPI2 && !SUMI && HAS_S) {
-        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // the last compensation MFMAs retired
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // margin: the last compensation MFMAs (8 needed, header)
 #pragma unroll
         for (int i = 0; i < G::RT; ++i)
 #pragma unroll
@@ -611,7 +638,7 @@ template <int BN, int TT, int KS> inline size_t mmq_ws_bytes(int M, int N) {
 
 template <int F, int BN, int TT, int W, bool P16, int NB = 2, int SB = 4, int KS = 1>
 inline bool mmq_shape_ok(const GemmArgs& g) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;  // the shape rules do not depend on OPT
     if (g.M < 1 || g.N < 1 || g.K % (QK * SB * KS) != 0) return false;
     if (KS > 1 && (g.sumi || !g.ws || g.ws_bytes < mmq_ws_bytes<BN, TT, KS>(g.M, g.N) || ((uintptr_t)g.ws & 255)))
         return false;
@@ -625,14 +652,14 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
 }
 
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1, bool EPI2 = false>
+          int KS = 1, bool EPI2 = false, int OPT = 0>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
-    using G = mmq_geom<F, BN, TT, W, P16, NB, SB>;
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB, OPT>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK, KS);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>;
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
-        describe_kernel(g, "mmq F=%d BN=%d TT=%d W=%d P16=%d NB=%d ABL=%d ROT=%d SB=%d KS=%d EPI2=%d grid=%ux%ux%u", F, BN,
-                        TT, W, (int)P16, NB, ABL, (int)ROT, SB, KS, (int)EPI2, grid.x, grid.y, grid.z);
+        describe_kernel(g, "mmq F=%d BN=%d TT=%d W=%d P16=%d NB=%d ABL=%d ROT=%d SB=%d KS=%d EPI2=%d OPT=%d grid=%ux%ux%u", F,
+                        BN, TT, W, (int)P16, NB, ABL, (int)ROT, SB, KS, (int)EPI2, OPT, grid.x, grid.y, grid.z);
         return hipSuccess;
     }
     unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;

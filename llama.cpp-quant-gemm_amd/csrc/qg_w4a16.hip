@@ -42,9 +42,10 @@ template <int F> __device__ __forceinline__ float w16_elem(uint32_t x, int j) {
 // its weights land (as the W4A8 GEMV's PRE / ONEU, qg_gemv_kernel.hpp), leaving only VALU work
 // once the weight bytes arrive.
 template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU = false>
+// (arguments the first loads need lead, within the 14 preloaded kernarg dwords: qg_gemv_kernel.hpp)
 __global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
-                                                       float* __restrict__ C, int M, int N, int K, long ldc_m,
-                                                       long ldc_n, long sA, long sC) {
+                                                       long sA, int M, int N, int K, float* __restrict__ C,
+                                                       long sC, long ldc_m, long ldc_n) {
     using G = w16_geom<F, BPL>;
     // chunk of <= MT activation rows
     A += blockIdx.y * sA;
@@ -615,8 +616,8 @@ hipError_t w16_launch(const GemmArgs& g, hipStream_t st) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kfn, grid, dim3(WGS), lds, st, (const float*)g.A, (const uint8_t*)g.B, g.C, g.M, g.N, g.K,
-                       g.ldc_m, g.ldc_n, (long)MT * g.K, (long)MT * g.ldc_m);
+    hipLaunchKernelGGL(kfn, grid, dim3(WGS), lds, st, (const float*)g.A, (const uint8_t*)g.B, (long)MT * g.K, g.M, g.N,
+                       g.K, g.C, (long)MT * g.ldc_m, g.ldc_m, g.ldc_n);
     return hipGetLastError();
 }
 

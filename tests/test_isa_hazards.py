@@ -1,0 +1,101 @@
+"""MFMA result hazard, checked on the shipped code object (CPU only).
+
+gfx950 needs 8 wait states between an MFMA and the first instruction that touches its destination
+registers with a non-MFMA instruction (VALU, LDS, memory): tools/mfma_hazard_probe.hip, run on
+an MI355X (profiles/r02_tuning/mfma_hazard_probe.txt), reads v_mfma_i32_16x16x32_i8 and
+v_mfma_f32_16x16x16_f16 results after exactly N states inside one asm string — wrong in all 64
+lanes at N <= 6, right from N = 8 — and hipcc pads exactly that (`s_nop 7`). The prefill kernel
+adds `s_nop 7; s_nop 7` of its own after its MFMA phases (qg_mmq_kernel.hpp). This test
+disassembles every gfx950 kernel in libqg_hip.so and asserts that no straight-line path from a
+v_mfma to an access of its destination has fewer than 8 wait states (s_nop N counts N + 1, any
+other instruction 1), so a compiler update that pads less fails here instead of in the sums.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "llama.cpp-quant-gemm_amd", "quant_gemm", "libqg_hip.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+REQUIRED = 8
+REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)(?!\w))")
+STOP = ("s_branch", "s_cbranch", "s_setpc", "s_endpgm", "s_barrier")
+
+
+def regs(text):
+    out = set()
+    for kind, lo, hi, one in REG.findall(text):
+        if one:
+            out.add((kind, int(one)))
+        else:
+            out.update((kind, r) for r in range(int(lo), int(hi) + 1))
+    return out
+
+
+@pytest.fixture(scope="module")
+def listing(tmp_path_factory):
+    if not (os.path.exists(OBJDUMP) and os.path.exists(LIB)):
+        pytest.skip("llvm-objdump or libqg_hip.so missing")
+    d = tmp_path_factory.mktemp("co")
+    so = shutil.copy(LIB, d / "libqg_hip.so")
+    subprocess.run([OBJDUMP, "--offloading", str(so)], cwd=d, capture_output=True, check=True)
+    text = []
+    for f in sorted(os.listdir(d)):
+        if "gfx950" in f:
+            text.append(subprocess.run([OBJDUMP, "-d", str(d / f)], capture_output=True, text=True, check=True).stdout)
+    assert text, "no gfx950 code object in libqg_hip.so"
+    return "\n".join(text)
+
+
+def instructions(listing):
+    """(function, [instruction text]) for every kernel."""
+    fn, body = None, []
+    for line in listing.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            if fn:
+                yield fn, body
+            fn, body = m.group(1), []
+            continue
+        ins = line.strip().split("//")[0].strip()
+        if fn and ins:
+            body.append(ins)
+    if fn:
+        yield fn, body
+
+
+def test_mfma_results_padded(listing):
+    checked, violations, mfmas = 0, [], 0
+    for fn, body in instructions(listing):
+        for i, ins in enumerate(body):
+            if not ins.startswith("v_mfma"):
+                continue
+            mfmas += 1
+            ops = ins.split(None, 1)[1]
+            dst = regs(ops.split(",")[0])
+            states = 0
+            for nxt in body[i + 1:]:
+                op = nxt.split()[0]
+                if op.startswith(STOP):
+                    break
+                touched = regs(nxt.split(None, 1)[1]) if " " in nxt else set()
+                if touched & dst:
+                    if op.startswith("v_mfma"):
+                        # MFMA -> MFMA dependencies (accumulator chains, operand forwarding) are the
+                        # matrix pipe's own interlock and hipcc's; once another MFMA rewrites these
+                        # registers, later readers belong to it (checked from its own position)
+                        if regs(nxt.split(None, 1)[1].split(",")[0]) & dst:
+                            break
+                    else:
+                        checked += 1
+                        if states < REQUIRED:
+                            violations.append(f"{fn}: {ins} -> {nxt} after {states} wait states")
+                        break
+                m = re.match(r"s_nop\s+(\d+)", nxt)
+                states += int(m.group(1)) + 1 if m else 1
+    assert mfmas > 100, "expected the prefill / W4A16 MFMA kernels in the library"
+    assert checked > mfmas // 4, (checked, mfmas)
+    assert not violations, "\n".join(violations[:20])
