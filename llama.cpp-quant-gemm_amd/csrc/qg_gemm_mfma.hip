@@ -25,9 +25,14 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
 // 108.9 -> 96.5 (the 4-wave 32 x 32 tiles with the two-workgroups-per-CU register cap)
 // The sumi parity hook runs the same instantiation with SUMI = true (the EPI2 form's own operand
 // fragments and MFMAs; only the final accumulate becomes a store of each block's int32 dot).
+// The short-argument entry (mmq1_kernel) where measured faster: 16-row tiles (M <= 16: -0.08..-0.10
+// us) and the 8-wave 32 x 32 tiles (M = 64 / 96: -0.2 us); the 32 x 16 8-wave tile (M = 32) and
+// the 4-wave tiles keep the general entry (+0.05..+0.55 us with the short one; ab_sig3.txt).
+template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8) || (BN == 32 && TT == 2 && W == 8);
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
-    if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true>(g, st);
-    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true>(g, st);
+    constexpr bool S = short_sig<BN, TT, W>;
+    if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true, 0, S>(g, st);
+    return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true, 0, S>(g, st);
 }
 
 template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hipStream_t st) {

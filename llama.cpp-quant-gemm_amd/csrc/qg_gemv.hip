@@ -7,6 +7,11 @@
 // The fused-quantization variants (AIN_F32 / AIN_F16_FUSED) share the configuration.
 #include "qg_gemv_kernel.hpp"
 
+// Workgroup size of the M = 1 loop-free GEMV (tuning knob for A/B builds; 1024 = product).
+#ifndef QG_GEMV1_WGS
+#define QG_GEMV1_WGS 1024
+#endif
+
 namespace qg {
 
 namespace {
@@ -26,6 +31,7 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
                 return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
             // activation records preloaded into registers for M <= 4 (tools/gemv_pre_probe.hip,
             // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
+            if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, QG_GEMV1_WGS, SUMI, AIN, false, true>(g, st);
             return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN, false, true>(g, st);
         }
     }

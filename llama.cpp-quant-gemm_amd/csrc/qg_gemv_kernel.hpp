@@ -220,11 +220,15 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // first 14 dwords, which the dispatch preloads into SGPRs (-amdgpu-kernarg-preload-count, Makefile);
 // the rest (output pointer and strides, the sumi hook) is fetched by an s_load that is only waited
 // for at the store, so no kernarg fetch sits in front of the weight stream.
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
-          bool ONEU = false>
-__global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                   long sA, long sB, int M, int N, int K, float* __restrict__ C,
-                                                   long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
+// ABL (tuning probes only; the product uses 0): bit 1 — no activation staging (records taken from a
+// constant: no A loads, no LDS, no barrier); bit 2 — no dot / epilogue (the weight dwords are summed);
+// bit 4 — nontemporal output stores; bit 8 — write-through (agent-scope, sc1) output stores.
+// The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
+// minimal argument list.
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL>
+__device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
+                                          int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
+                                          int32_t* __restrict__ sumi_out) {
     using G = gemv_geom<F, BPL>;
     QG_STAMP(t0);
     QG_CLK(c0);
@@ -268,7 +272,9 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
     // 1) activation block loads of this thread (one thread per block), the first before the
     //    weight stream; 2) the lane's first weight unit; 3) LDS records
     const int totb = M * nb;
-    if constexpr (AIN == AIN_Q8_1) {
+    if constexpr ((ABL & 1) != 0) {
+        load_unit(cur, lir);
+    } else if constexpr (AIN == AIN_Q8_1) {
         uint32_t ab[9];
         auto load_ablk = [&](int g) {
             const uint32_t* p = A + (long)g * 9;
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
             make_act_record<F>(w, lds + rec_of(g));
         }
     }
-    __syncthreads();
+    if constexpr ((ABL & 1) == 0) __syncthreads();
     QG_STAMP(tb);
     QG_WAIT_STAMP(t1);
 
@@ -312,7 +318,10 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
                 for (int m = 0; m < MT; ++m) {
                     const uint32_t* rec = lds + (min(m, M - 1) * U + u) * G::REC_DW + bi * 12;
 #pragma unroll
-                    for (int x = 0; x < 3; ++x) pre[bi][m][x] = *reinterpret_cast<const uint4*>(rec + 4 * x);
+                    for (int x = 0; x < 3; ++x) {
+                        if constexpr ((ABL & 1) != 0) pre[bi][m][x] = make_uint4(0x11u * (x + 1), 0x1234u, (uint32_t)u, 0x3F800000u);
+                        else pre[bi][m][x] = *reinterpret_cast<const uint4*>(rec + 4 * x);
+                    }
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -329,6 +338,13 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
                         a[0] = *reinterpret_cast<const uint4*>(rec);
                         a[1] = *reinterpret_cast<const uint4*>(rec + 4);
                         a[2] = *reinterpret_cast<const uint4*>(rec + 8);
+                    }
+                    if constexpr ((ABL & 2) != 0) {
+                        uint32_t x = a[2].w;
+#pragma unroll
+                        for (int v = 0; v < G::UDW; ++v) x += cur[v];
+                        acc[m] += __uint_as_float(x & 0x3FFFFFFFu);
+                        continue;
                     }
                     const uint32_t d = block_dot<F, bi>(cur, a);
                     if constexpr (SUMI) {
@@ -362,12 +378,46 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
         if (row_ok && lir == LPR - 1) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-                if (m < M) C[m * ldc_m + row * ldc_n] = acc[m];
+                if (m < M) {
+                    if constexpr ((ABL & 4) != 0) __builtin_nontemporal_store(acc[m], C + m * ldc_m + row * ldc_n);
+                    else if constexpr ((ABL & 8) != 0)
+                        __hip_atomic_store(C + m * ldc_m + row * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else C[m * ldc_m + row * ldc_n] = acc[m];
+                }
         }
     }
     QG_STAMP(t2);
     QG_CLK(c2);
     QG_STAMP_STORE(t0, tb, t1, tc, t2, c0, c2);
+}
+
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
+          bool ONEU = false, int ABL = 0>
+__global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                   long sA, long sB, int M, int N, int K, float* __restrict__ C,
+                                                   long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
+    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, ONEU, ABL>(A, B, sA, sB, M, N, K, C, sC, ldc_m, ldc_n, sumi_out);
+}
+
+// M = 2..8, one product: (A, B, M, N, K, out, ldc_m, ldc_n) with 32-bit output strides = 10 dwords
+// (the general entry preloads 14 and s_loads the rest).
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool PRE = (MT <= 2), bool ONEU = false>
+__global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int M,
+                                                    int N, int K, void* __restrict__ out, int ldc_m, int ldc_n) {
+    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, false, PRE, ONEU, 0>(A, B, 0, 0, M, N, K, SUMI ? nullptr : (float*)out, 0,
+                                                                     ldc_m, ldc_n, SUMI ? (int32_t*)out : nullptr);
+}
+
+// M = 1, one product, out[n] (activation- and weight-major coincide at M = 1): the minimal argument
+// list (A, B, N, K, out) = 8 dwords, all preloaded into SGPRs. Each preloaded kernel-argument dword
+// costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
+// entry's 13 preloaded dwords than with these 8 (tools/gemv_direct_probe.hip,
+// profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
+template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
+__global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
+                                                    int K, void* __restrict__ out) {
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, 0>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+                                                                     1, SUMI ? (int32_t*)out : nullptr);
 }
 
 // Host side -------------------------------------------------------------------------------------
@@ -396,10 +446,37 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
     const bool one = g.K / QK / BPL <= LPR;
+    // M = 1, one product, unit output stride: the minimal-argument entry (gemv1_kernel)
+    const bool m1 = MT == 1 && PRE && !NT && g.M == 1 && g.batch == 1 && g.ldc_n == 1;
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
-        describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d grid=%dx%d", F, MT, BPL,
-                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (int)one, grid, g.batch);
+        describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (int)one,
+                        m1 ? "m1" : (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) ? "short" : "full", grid,
+                        g.batch);
         return hipSuccess;
+    }
+    if (m1) {
+        auto k1 = one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        void* out = SUMI ? (void*)g.sumi : (void*)g.C;
+        hipLaunchKernelGGL(k1, dim3(grid), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.N, g.K, out);
+        return hipGetLastError();
+    }
+    // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)
+    if (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) {
+        auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, true>
+                      : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), false>;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        void* out = SUMI ? (void*)g.sumi : (void*)g.C;
+        hipLaunchKernelGGL(ks, dim3(grid), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.M, g.N, g.K, out,
+                           (int)g.ldc_m, (int)g.ldc_n);
+        return hipGetLastError();
     }
     // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4)
     auto kfn = one ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>

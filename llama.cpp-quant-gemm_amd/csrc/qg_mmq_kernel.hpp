@@ -153,14 +153,10 @@ template <int NI> __device__ __forceinline__ void wait_stage(int younger) {
 // fixed-order partial tile goes to the workspace and the last slice to finish (agent-scope counter
 // per output tile) sums the KS partials in slice order (deterministic: the same order whichever
 // workgroup arrives last) and re-arms the counter to 0 for the next launch.
-template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1, bool EPI2 = false, int OPT = 0>
-// (4-wave workgroups: at least two per CU, i.e. <= 256 VGPRs — without the cap the EPI2 form took
-// 320 and ran one workgroup per CU, 13 % slower at M=512 than with it)
-__global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                     float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
-                                                     int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
-                                                     unsigned* __restrict__ cnt) {
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB, int ABL, bool ROT, int SB, int KS, bool EPI2, int OPT>
+__device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, float* __restrict__ C,
+                                         int32_t* __restrict__ sumi_out, int M, int N, int K, long ldc_m, long ldc_n,
+                                         float* __restrict__ part, unsigned* __restrict__ cnt) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB, OPT>;
     using T = wfmt<F>;
     constexpr bool ZL = (OPT & MMQ_ZL) != 0 && EPI2;
@@ -624,6 +620,32 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8
 #endif
 }
 
+// General entry (probes: split-K workspace, ablations).
+// (4-wave workgroups: at least two per CU, i.e. <= 256 VGPRs — without the cap the EPI2 form took
+// 320 and ran one workgroup per CU, 13 % slower at M=512 than with it)
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
+          int KS = 1, bool EPI2 = false, int OPT = 0>
+__global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                     float* __restrict__ C, int32_t* __restrict__ sumi_out, int M,
+                                                     int N, int K, long ldc_m, long ldc_n, float* __restrict__ part,
+                                                     unsigned* __restrict__ cnt) {
+    mmq_body<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>(A, B, C, sumi_out, M, N, K, ldc_m, ldc_n, part, cnt);
+}
+
+// Short entry (no split-K): (A, B, M, N, K, out, ldc_m, ldc_n) with 32-bit output strides = 10
+// kernel-argument dwords, all preloaded into SGPRs (each preloaded dword costs every wave's launch:
+// qg_gemv_kernel.hpp, gemv1_kernel). SUMI: out is the parity hook's int32 buffer. Faster for the
+// 16-row and the 32 x 32 8-wave tiles, slower for the 32 x 16 8-wave and the 4-wave tiles
+// (profiles/r02_tuning/ab_sig2.txt, ab_sig3.txt), so the dispatch picks it per tile.
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int SB = 4, bool EPI2 = false, int OPT = 0>
+__global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmq1_kernel(const uint8_t* __restrict__ A,
+                                                      const uint8_t* __restrict__ B, int M, int N, int K,
+                                                      void* __restrict__ out, int ldc_m, int ldc_n) {
+    mmq_body<F, BN, TT, W, SUMI, P16, NB, 0, false, SB, 1, EPI2, OPT>(A, B, SUMI ? nullptr : (float*)out,
+                                                                       SUMI ? (int32_t*)out : nullptr, M, N, K, ldc_m, ldc_n,
+                                                                       nullptr, nullptr);
+}
+
 // Preconditions: K a multiple of 128 (whole stages), 16-B aligned activation rows and base, weight
 // rows and stages aligned to the DMA piece, one workgroup's rows / tokens within 2 GiB (tensors of
 // any size otherwise). P16 additionally: a 16-B aligned B
@@ -648,20 +670,50 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     if (((uintptr_t)g.B % G::WPS) != 0 || RB % G::WPS != 0) return false;
     // per-lane DMA offsets are 32-bit relative to the workgroup's 64-bit row / token base
     if (RB * BN >= (1L << 31) || AB * G::NTOK >= (1L << 31)) return false;
+    if (g.ldc_m > INT32_MAX || g.ldc_n > INT32_MAX) return false;  // mmq1_kernel's 32-bit strides
     return true;
 }
 
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB, int ABL, bool ROT, int SB, int KS, bool EPI2, int OPT>
+hipError_t mmq_launch_full(const GemmArgs& g, hipStream_t st, dim3 grid);
+
+// SHORT: launch through mmq1_kernel (10 preloaded argument dwords) instead of the general entry —
+// per configuration, as measured (qg_gemm_mfma.hip).
 template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB = 2, int ABL = 0, bool ROT = false, int SB = 4,
-          int KS = 1, bool EPI2 = false, int OPT = 0>
+          int KS = 1, bool EPI2 = false, int OPT = 0, bool SHORT = false>
 hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     using G = mmq_geom<F, BN, TT, W, P16, NB, SB, OPT>;
     const dim3 grid((g.N + BN - 1) / BN, (g.M + G::NTOK - 1) / G::NTOK, KS);
-    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>;
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
-        describe_kernel(g, "mmq F=%d BN=%d TT=%d W=%d P16=%d NB=%d ABL=%d ROT=%d SB=%d KS=%d EPI2=%d OPT=%d grid=%ux%ux%u", F,
-                        BN, TT, W, (int)P16, NB, ABL, (int)ROT, SB, KS, (int)EPI2, OPT, grid.x, grid.y, grid.z);
+        const bool short_sig = SHORT && KS == 1 && ABL == 0 && !ROT;
+        describe_kernel(g, "mmq F=%d BN=%d TT=%d W=%d P16=%d NB=%d ABL=%d ROT=%d SB=%d KS=%d EPI2=%d OPT=%d SIG=%s grid=%ux%ux%u",
+                        F, BN, TT, W, (int)P16, NB, ABL, (int)ROT, SB, KS, (int)EPI2, OPT, short_sig ? "short" : "full", grid.x,
+                        grid.y, grid.z);
         return hipSuccess;
     }
+    if constexpr (SHORT && KS == 1 && ABL == 0 && !ROT) {  // (mmq_shape_ok: 32-bit output strides)
+        auto k1 = mmq1_kernel<F, BN, TT, W, SUMI, P16, NB, SB, EPI2, OPT>;
+        if (G::LDS > 64 * 1024) {
+            static bool attr1_set = false;  // once per instantiation (not a stream op: capture-safe)
+            if (!attr1_set) {
+                hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+                if (e != hipSuccess) return e;
+                attr1_set = true;
+            }
+        }
+        void* out = SUMI ? (void*)g.sumi : (void*)g.C;
+        hipLaunchKernelGGL(k1, grid, dim3(W * 64), G::LDS, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.M, g.N, g.K, out,
+                           (int)g.ldc_m, (int)g.ldc_n);
+        return hipGetLastError();
+    } else {
+        return mmq_launch_full<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>(g, st, grid);
+    }
+}
+
+template <int F, int BN, int TT, int W, bool SUMI, bool P16, int NB, int ABL, bool ROT, int SB, int KS, bool EPI2, int OPT>
+hipError_t mmq_launch_full(const GemmArgs& g, hipStream_t st, dim3 grid) {
+    using G = mmq_geom<F, BN, TT, W, P16, NB, SB, OPT>;
+    auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>;
     unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;
     float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
     if (G::LDS > 64 * 1024) {

@@ -41,11 +41,10 @@ template <int F> __device__ __forceinline__ float w16_elem(uint32_t x, int j) {
 // the lane's activation records are read into registers right after the staging barrier, before
 // its weights land (as the W4A8 GEMV's PRE / ONEU, qg_gemv_kernel.hpp), leaving only VALU work
 // once the weight bytes arrive.
-template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU = false>
-// (arguments the first loads need lead, within the 14 preloaded kernarg dwords: qg_gemv_kernel.hpp)
-__global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
-                                                       long sA, int M, int N, int K, float* __restrict__ C,
-                                                       long sC, long ldc_m, long ldc_n) {
+// The body is shared by the general entry and the M = 1 one with the minimal argument list (below).
+template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU>
+__device__ __forceinline__ void w16_gemv_body(const float* __restrict__ A, const uint8_t* __restrict__ B, long sA, int M,
+                                              int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n) {
     using G = w16_geom<F, BPL>;
     // chunk of <= MT activation rows
     A += blockIdx.y * sA;
@@ -165,6 +164,22 @@ __global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__
         for (int m = 0; m < MT; ++m)
             if (m < M) C[m * ldc_m + row * ldc_n] = acc[m];
     }
+}
+
+// (arguments the first loads need lead, within the 14 preloaded kernarg dwords: qg_gemv_kernel.hpp)
+template <int F, int MT, int BPL, int LPR, int WGS, bool ONEU = false>
+__global__ __launch_bounds__(WGS) void w16_gemv_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
+                                                       long sA, int M, int N, int K, float* __restrict__ C,
+                                                       long sC, long ldc_m, long ldc_n) {
+    w16_gemv_body<F, MT, BPL, LPR, WGS, ONEU>(A, B, sA, M, N, K, C, sC, ldc_m, ldc_n);
+}
+
+// M = 1, unit output stride: (A, B, N, K, C) = 8 preloaded argument dwords (as the W4A8 GEMV's
+// gemv1_kernel, qg_gemv_kernel.hpp: every preloaded dword costs each wave's launch)
+template <int F, int BPL, int LPR, int WGS, bool ONEU = false>
+__global__ __launch_bounds__(WGS) void w16_gemv1_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B, int N,
+                                                        int K, float* __restrict__ C) {
+    w16_gemv_body<F, 1, BPL, LPR, WGS, ONEU>(A, B, 0, 1, N, K, C, 0, 0, 1);
 }
 
 // Any K % 32 == 0 and alignment: one wave per output element, lanes stride over blocks.
@@ -611,6 +626,17 @@ hipError_t w16_launch(const GemmArgs& g, hipStream_t st) {
     const int rows = g.M < MT ? g.M : MT;
     const size_t lds = w16_lds<F, BPL>(rows, g.K);
     const dim3 grid((g.N + RPB - 1) / RPB, (g.M + MT - 1) / MT);
+    if constexpr (MT == 1) {
+        if (g.M == 1 && g.ldc_n == 1) {
+            auto k1 = w16_gemv1_kernel<F, BPL, LPR, WGS, ONEU>;
+            if (lds > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(k1, dim3(grid.x), dim3(WGS), lds, st, (const float*)g.A, (const uint8_t*)g.B, g.N, g.K, g.C);
+            return hipGetLastError();
+        }
+    }
     auto kfn = w16_gemv_kernel<F, MT, BPL, LPR, WGS, ONEU>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -138,16 +138,100 @@ hipError_t gemv_direct_launch(const GemmArgs& g, hipStream_t st) {
 }  // namespace qg
 
 // pure read of the weights in the direct kernel's shape: lane (row, u) reads its UB-byte unit
-template <int UB, int WGS>
+// ST: 0 no store (unless a magic value), 1 one plain store per row (lane 63), 2 nontemporal,
+// 3 agent-scope write-through (sc1), 4 DPP row sum + plain store (the GEMV's tail)
+template <int UB, int WGS, int ST = 0>
 __global__ __launch_bounds__(WGS) void unit_read(const uint8_t* __restrict__ B, int N, int U, float* out) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * (WGS / 64) + (threadIdx.x >> 6);
     if (row >= N) return;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(B + ((long)row * U + (lane < U ? lane : 0)) * UB);
+    if constexpr (ST == 9) if (lane == 63) out[row] = (float)row;  // the row's store at the START
     uint32_t acc = 0;
 #pragma unroll
     for (int v = 0; v < UB / 4; ++v) acc ^= p[v];
-    if (acc == 0x12345678u) out[row] = 1.0f;
+    if constexpr (ST == 0) {
+        if (acc == 0x12345678u) out[row] = 1.0f;
+    } else {
+        float f = __uint_as_float(acc & 0x3FFFFFFFu);
+        if constexpr (ST == 4 || ST == 5 || ST == 7 || ST == 8 || ST == 9) f = group_sum_last<64>(f);
+        if constexpr (ST == 9) {
+            if (f == 1.2345f) out[row] = f;
+            return;
+        }
+        if constexpr (ST == 7) {  // one real store in the whole grid (row 0), the rest magic-guarded
+            if (lane == 63 && (row == 0 || f == 1.2345f)) out[row] = f;
+            return;
+        }
+        if constexpr (ST == 8) {  // one store per workgroup (its first row)
+            if (lane == 63 && ((row & (WGS / 64 - 1)) == 0 || f == 1.2345f)) out[row] = f;
+            return;
+        }
+        if constexpr (ST == 5) {  // DPP sum, no real store
+            if (f == 1.2345f) out[row] = f;
+            return;
+        }
+        if constexpr (ST == 6) {  // no reduction: every lane stores its own value to the row's slot
+            out[row] = f;
+            return;
+        }
+        if (lane == 63) {
+            if constexpr (ST == 2) __builtin_nontemporal_store(f, out + row);
+            else if constexpr (ST == 3) __hip_atomic_store(out + row, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else out[row] = f;
+        }
+    }
+}
+
+// the pure read + DPP + store with the product GEMV's kernel signature (13 arguments: the first 14
+// dwords preloaded into SGPRs, the rest fetched by s_load)
+template <int UB, int WGS>
+__global__ __launch_bounds__(WGS) void unit_read_sig(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA,
+                                                     long sB, int M, int N, int K, float* __restrict__ C, long sC,
+                                                     long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (WGS / 64) + (threadIdx.x >> 6);
+    const int U = K / 64;
+    if (row >= N) return;
+    B += blockIdx.y * sB;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(B + ((long)row * U + (lane < U ? lane : 0)) * UB);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int v = 0; v < UB / 4; ++v) acc ^= p[v];
+    float f = group_sum_last<64>(__uint_as_float(acc & 0x3FFFFFFFu));
+    if (lane == 63) C[row * ldc_n] = f;
+}
+
+// signature probes: V = 1: (A, B, N, K, C) — 8 dwords, all preloaded; V = 2: (A, B, sA, sB, M, N, K, C) —
+// 13 dwords, all preloaded, no s_load
+template <int UB, int WGS>
+__global__ __launch_bounds__(WGS) void unit_read_v1(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
+                                                    int K, float* __restrict__ C) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (WGS / 64) + (threadIdx.x >> 6);
+    const int U = K / 64;
+    if (row >= N) return;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(B + ((long)row * U + (lane < U ? lane : 0)) * UB);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int v = 0; v < UB / 4; ++v) acc ^= p[v];
+    float f = group_sum_last<64>(__uint_as_float(acc & 0x3FFFFFFFu));
+    if (lane == 63) C[row] = f;
+}
+template <int UB, int WGS>
+__global__ __launch_bounds__(WGS) void unit_read_v2(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA,
+                                                    long sB, int M, int N, int K, float* __restrict__ C) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (WGS / 64) + (threadIdx.x >> 6);
+    const int U = K / 64;
+    if (row >= N) return;
+    B += blockIdx.y * sB;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(B + ((long)row * U + (lane < U ? lane : 0)) * UB);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int v = 0; v < UB / 4; ++v) acc ^= p[v];
+    float f = group_sum_last<64>(__uint_as_float(acc & 0x3FFFFFFFu));
+    if (lane == 63) C[row] = f;
 }
 
 static uint16_t f2h(float f) { _Float16 h = (_Float16)f; uint16_t b; memcpy(&b, &h, 2); return b; }
@@ -265,9 +349,40 @@ static void run_shape(int F, int M, int N, int K, std::vector<Variant>& vs, hipS
     CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
 }
 
+// the product's M = 1 loop-free kernel with its ABL ablation bits (qg_gemv_kernel.hpp)
+template <int F, int ABL> static hipError_t abl_launch(const GemmArgs& g, hipStream_t st) {
+    const size_t lds = (ABL & 1) ? 0 : gemv_lds_bytes<F, 2>(g.M, g.K);
+    hipLaunchKernelGGL((gemv_kernel<F, 1, 2, 64, 1024, false, AIN_Q8_1, false, true, true, ABL>), dim3((g.N + 15) / 16, 1),
+                       dim3(1024), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.sA, g.sB, g.M, g.N, g.K, g.C, g.sC,
+                       g.ldc_m, g.ldc_n, g.sumi);
+    return hipGetLastError();
+}
+
 template <int F, int MT> static std::vector<Variant> variants(bool with_read) {
     std::vector<Variant> vs;
     vs.push_back({"staged bpl2 lpr64 wg1024 (product)", gemv_launch<F, MT, 2, 64, 1024, false, AIN_Q8_1, false, true>, false});
+    if (MT == 1 && getenv("QG_ABL")) {
+        vs.push_back({"product, neither (staging, dot)", abl_launch<F, 3>, false});
+        vs.push_back({"product, nt stores", abl_launch<F, 4>, false});
+        vs.push_back({"product, sc1 stores", abl_launch<F, 8>, false});
+        vs.push_back({"product, neither + nt stores", abl_launch<F, 7>, false});
+        constexpr int UB = 2 * wfmt<F>::BB;
+#define RD(ST, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { \
+            hipLaunchKernelGGL((unit_read<UB, 1024, ST>), dim3((g.N + 15) / 16), dim3(1024), 0, s, (const uint8_t*)g.B, g.N, g.K / 64, g.C); \
+            return hipGetLastError(); }, true});
+        RD(0, "pure read (no store)")
+        RD(4, "pure read + DPP sum + store")
+        RD(5, "pure read + DPP sum, no store")
+        RD(6, "pure read + 64-lane store, no DPP")
+        RD(7, "pure read + DPP, ONE store per grid")
+        RD(8, "pure read + DPP, one store per WG")
+        RD(9, "pure read + DPP, per-row store at START")
+        vs.push_back({"pure read + DPP + store, product signature", [](const GemmArgs& g, hipStream_t s) {
+            hipLaunchKernelGGL((unit_read_sig<UB, 1024>), dim3((g.N + 15) / 16), dim3(1024), 0, s, (const uint32_t*)g.A,
+                               (const uint8_t*)g.B, g.sA, g.sB, g.M, g.N, g.K, g.C, g.sC, g.ldc_m, g.ldc_n, g.sumi);
+            return hipGetLastError(); }, true});
+#undef RD
+    }
     vs.push_back({"direct bpl2 lpr64 wg1024", gemv_direct_launch<F, MT, 2, 64, 1024, false>, false});
     vs.push_back({"direct bpl2 lpr64 wg512", gemv_direct_launch<F, MT, 2, 64, 512, false>, false});
     vs.push_back({"direct bpl2 lpr64 wg256", gemv_direct_launch<F, MT, 2, 64, 256, false>, false});
@@ -284,6 +399,14 @@ template <int F, int MT> static std::vector<Variant> variants(bool with_read) {
                           hipLaunchKernelGGL((unit_read<UB, 256>), dim3((g.N + 3) / 4), dim3(256), 0, s,
                                              (const uint8_t*)g.B, g.N, g.K / 64, g.C);
                           return hipGetLastError(); }, true});
+        vs.push_back({"read+DPP+store, sig (A,B,N,K,C)", [](const GemmArgs& g, hipStream_t s) {
+            hipLaunchKernelGGL((unit_read_v1<UB, 1024>), dim3((g.N + 15) / 16), dim3(1024), 0, s, (const uint32_t*)g.A,
+                               (const uint8_t*)g.B, g.N, g.K, g.C);
+            return hipGetLastError(); }, true});
+        vs.push_back({"read+DPP+store, sig 13 dw preloaded", [](const GemmArgs& g, hipStream_t s) {
+            hipLaunchKernelGGL((unit_read_v2<UB, 1024>), dim3((g.N + 15) / 16), dim3(1024), 0, s, (const uint32_t*)g.A,
+                               (const uint8_t*)g.B, g.sA, g.sB, g.M, g.N, g.K, g.C);
+            return hipGetLastError(); }, true});
     }
     return vs;
 }
@@ -292,6 +415,7 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     { auto v = variants<FMT_Q4_0, 1>(true); run_shape(FMT_Q4_0, 1, 4096, 4096, v, st); }
+    if (getenv("QG_ABL")) return 0;
     { auto v = variants<FMT_Q4_0, 1>(false); run_shape(FMT_Q4_0, 1, 4000, 4096, v, st); }
     { auto v = variants<FMT_Q4_0, 2>(false); run_shape(FMT_Q4_0, 2, 4096, 4096, v, st); }
     { auto v = variants<FMT_Q4_1, 1>(true); run_shape(FMT_Q4_1, 1, 4096, 4096, v, st); }
