@@ -144,6 +144,16 @@ template <int G> __device__ __forceinline__ float group_sum_last(float x) {
     return x;
 }
 
+// XCD-aware tile order. Workgroups of a launch are placed round-robin over the 8 XCDs (linear
+// workgroup b on XCD b % 8); for a grid of G tiles along x this gives XCD x the contiguous tile range
+// [x*(G/8) + min(x, G%8), ...) (a bijection on 0..G-1), so neighbouring tiles — and the output lines
+// they share — stay in one XCD's L2. Only for grids of one dispatch round: with many rounds the
+// linear order streams better (qg_gemv_kernel.hpp).
+__device__ __forceinline__ int xcd_tile(int b, int G) {
+    const int g8 = G >> 3, r8 = G & 7, x = b & 7;
+    return x * g8 + min(x, r8) + (b >> 3);
+}
+
 // Per-block fp32 term, operation order as in the reference (see header comment).
 // fs = (float)sumi (exact: |sumi| < 2^24).
 template <int F> __device__ __forceinline__ float block_term_f(float fs, float dw, float mw, float da, float sa) {

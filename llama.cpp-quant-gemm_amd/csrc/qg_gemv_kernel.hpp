@@ -244,7 +244,14 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int lir = lane % LPR;
-    const int row = blockIdx.x * RPB + (tid >> 6) * RPW + lane / LPR;
+    // XCD-aware tile order for grids of one dispatch round (<= 512 workgroups): workgroups are placed
+    // round-robin over the 8 XCDs (b -> XCD b % 8), and XCD x takes a contiguous range of row tiles,
+    // so the 64-B output pieces of neighbouring workgroups dirty whole lines of ONE XCD's L2 (the
+    // end-of-kernel write-back is the GEMV's largest fixed cost after the launch;
+    // profiles/r02_tuning/ab_xcd.txt: M=1 3.33 -> 3.29 us, M=2 3.66 -> 3.58). Larger grids keep
+    // the linear order (N=32000: 12.55 us linear, 13.28 remapped).
+    const int tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int row = tile * RPB + (tid >> 6) * RPW + lane / LPR;
     const bool row_ok = row < N;
 
     const uint8_t* wrow = B + (long)(row_ok ? row : 0) * ((long)U * G::UB);

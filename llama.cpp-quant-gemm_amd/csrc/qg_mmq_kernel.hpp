@@ -167,7 +167,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     const int lane = threadIdx.x & 63;
     const int r16 = lane & 15;
     const int q = lane >> 4;
-    const int n0 = blockIdx.x * BN;
+const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * G::NTOK;
     const int nb = K / QK;
     const int H = nb / SB / KS;  // stages of this workgroup's K slice

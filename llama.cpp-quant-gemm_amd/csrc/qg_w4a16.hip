@@ -59,7 +59,7 @@ __device__ __forceinline__ void w16_gemv_body(const float* __restrict__ A, const
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int lir = lane % LPR;
-    const int row = blockIdx.x * RPB + (tid >> 6) * RPW + lane / LPR;
+const int row = blockIdx.x * RPB + (tid >> 6) * RPW + lane / LPR;
     const bool row_ok = row < N;
 
     // 1) first activation float4s in flight, 2) this lane's first weight unit, 3) stage to LDS

@@ -4,7 +4,7 @@
 weight copies (> 600 MB, so every launch streams from HBM) captured in a hipGraph, HIP events on
 the launch stream — in interleaved rounds, so box-to-box noise cancels.
 
-  python tools/ab_lib.py --libs a.so b.so [--shapes 1x4096x4096:2,32x4096x4096:2] [--rounds 7]
+  python tools/ab_lib.py --libs a.so b.so [--shapes 1x4096x4096:2,32x4096x4096:2] [--rounds 7] [--w16]
 Outputs must agree bit for bit across the libraries (checked on every shape).
 """
 from __future__ import annotations
@@ -30,6 +30,8 @@ def load(path: str) -> ctypes.CDLL:
     lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
     lib.qg_gemm_w4a8_ex.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     lib.qg_gemm_w4a8_ex.restype = ctypes.c_int
+    lib.qg_gemm_w4a16.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    lib.qg_gemm_w4a16.restype = ctypes.c_int
     return lib
 
 
@@ -41,6 +43,7 @@ def main() -> None:
     ap.add_argument("--G", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--w16", action="store_true", help="time qg_gemm_w4a16 (fp32 activations, Q4_0 weights)")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     dev = torch.device("cuda", 0)
@@ -50,7 +53,8 @@ def main() -> None:
         wt = int(wt)
         gen = torch.Generator(device=dev)
         gen.manual_seed(M * 7 + N)
-        aq = qg.quantize_q8_1(torch.rand((M, K), generator=gen, device=dev) * 2 - 1)
+        af = torch.rand((M, K), generator=gen, device=dev) * 2 - 1
+        aq = af if a.w16 else qg.quantize_q8_1(af)
         wq = qg.quantize(torch.rand((N, K), generator=gen, device=dev) * 2 - 1, wt)
         R = max(a.G, math.ceil(600e6 / wq.numel()))
         copies = torch.empty((R,) + tuple(wq.shape), dtype=torch.uint8, device=dev)
@@ -60,8 +64,12 @@ def main() -> None:
         for li, lib in enumerate(libs):
             def step(st, li=li, lib=lib):
                 for j in range(a.G):
-                    rc = lib.qg_gemm_w4a8_ex(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
-                                             P(outs[li, j].data_ptr()), M, N, K, wt, a.algo, st)
+                    if a.w16:
+                        rc = lib.qg_gemm_w4a16(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
+                                               P(outs[li, j].data_ptr()), M, N, K, st)
+                    else:
+                        rc = lib.qg_gemm_w4a8_ex(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
+                                                 P(outs[li, j].data_ptr()), M, N, K, wt, a.algo, st)
                     assert rc == 0, rc
             side = torch.cuda.Stream()
             with torch.cuda.stream(side):
@@ -87,7 +95,7 @@ def main() -> None:
                 times[li].append(e0.elapsed_time(e1) * 1e3 / (a.reps * a.G))
         nb = K // 32
         bb = qg.BLOCK_BYTES[wt]
-        nbytes = N * nb * bb + M * nb * 36 + M * N * 4
+        nbytes = N * nb * bb + M * K * (4 if a.w16 else 36 / 32) + M * N * 4
         print(f"M={M} N={N} K={K} wtype={wt} ({nbytes} B/launch, {R} copies)")
         for li, p in enumerate(a.libs):
             med = statistics.median(times[li])
