@@ -30,8 +30,8 @@ def load(path: str) -> ctypes.CDLL:
     lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
     lib.qg_gemm_w4a8_ex.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     lib.qg_gemm_w4a8_ex.restype = ctypes.c_int
-    lib.qg_gemm_w4a16.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
-    lib.qg_gemm_w4a16.restype = ctypes.c_int
+    lib.qg_gemm_w4a16_ws.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_size_t, P]
+    lib.qg_gemm_w4a16_ws.restype = ctypes.c_int
     return lib
 
 
@@ -61,12 +61,14 @@ def main() -> None:
         copies.copy_(wq.unsqueeze(0).expand_as(copies))
         outs = torch.empty((len(libs), a.G, M, N), dtype=torch.float32, device=dev)
         graphs = []
+        WSB = 64 << 20  # W4A16: each library's own caller workspace (zeroed once), capture-safe
+        wss = [torch.zeros(WSB // 4, dtype=torch.int32, device=dev) for _ in libs] if a.w16 else []
         for li, lib in enumerate(libs):
             def step(st, li=li, lib=lib):
                 for j in range(a.G):
                     if a.w16:
-                        rc = lib.qg_gemm_w4a16(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
-                                               P(outs[li, j].data_ptr()), M, N, K, st)
+                        rc = lib.qg_gemm_w4a16_ws(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
+                                                  P(outs[li, j].data_ptr()), M, N, K, P(wss[li].data_ptr()), WSB, st)
                     else:
                         rc = lib.qg_gemm_w4a8_ex(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
                                                  P(outs[li, j].data_ptr()), M, N, K, wt, a.algo, st)
@@ -102,7 +104,7 @@ def main() -> None:
             print(f"  {os.path.basename(p):28s} {med:7.3f} us  (min {min(times[li]):.3f} max {max(times[li]):.3f})"
                   f"  {nbytes / med / 1e3:7.1f} GB/s  frac {nbytes / med / 8e6:.3f}")
         sys.stdout.flush()
-        del copies, outs, graphs
+        del copies, outs, graphs, wss
 
 
 if __name__ == "__main__":
