@@ -816,7 +816,8 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
 // right after the barrier that follows its last reader). After the raw activation planes of stage s
 // have landed, the workgroup splits them once (w16s_split) into the planes buffer, a second barrier
 // publishes it, and every wave computes the stage. ABL (tuning probes only): 1 = DMA and waits
-// without split / compute, 2 = split + compute on whatever the LDS holds, no DMA.
+// without split / compute, 2 = split + compute on whatever the LDS holds, no DMA, 3 = neither (the
+// launch, barriers and the split-K hand-off alone).
 template <int R, int ABL>
 __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int M, int N, int K, long ldc_m, long ldc_n,
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
     }
     auto slot = [&](int s) { return lds + (s % R) * SBYTES; };
     auto issue = [&](int s) {
-        if constexpr (ABL == 2) return;
+        if constexpr (ABL >= 2) return;
         const int h = h0 + s;
         const long dw = (long)h * RSB - ((h & 1) ? 8 : 0), da = (long)h * 512;
         uint8_t* dst = slot(s) + 1024 * wave;
@@ -863,11 +864,11 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
     f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
     for (int s = 0; s < nloc; ++s) {
         // stages issued so far: 0 .. min(nloc, s + AHEAD) - 1; wait for stage s
-        if constexpr (ABL != 2) w16s_wait(min(nloc, s + AHEAD) - 1 - s);
+        if constexpr (ABL < 2) w16s_wait(min(nloc, s + AHEAD) - 1 - s);
         __builtin_amdgcn_s_barrier();  // stage s landed everywhere; stage s - 1 and the planes are free
         asm volatile("" ::: "memory");
         if (s + AHEAD < nloc) issue(s + AHEAD);  // into the slot of stage s - 1
-        if constexpr (ABL != 1) {
+        if constexpr (ABL != 1 && ABL != 3) {
             w16s_split(slot(s), planes, wave, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // planes of stage s published
@@ -905,21 +906,28 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
         *last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)KS - 1;
     __syncthreads();
     if (!*last) return;
-    // slice-order sum: 4 slices' loads in flight per round
+    // slice-order sum, up to 8 slices' loads in flight per round; this slice's own partial from registers
+    constexpr int RS = 8;
+    const int z = blockIdx.z;
     f32x4_t v[2];
-    for (int s0 = 0; s0 < KS; s0 += 4) {
-        f32x4_t x[4][2];
+    for (int s0 = 0; s0 < KS; s0 += RS) {
+        f32x4_t x[RS][2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < RS; ++j)
+            if (s0 + j < KS && s0 + j != z) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) x[j][i] = ld_x4_sc1(pt + min(s0 + j, KS - 1) * PT + pidx(i));
+                for (int i = 0; i < 2; ++i) x[j][i] = ld_x4_sc1(pt + (s0 + j) * PT + pidx(i));
+            } else {
+                x[j][0] = acc[0];
+                x[j][1] = acc[1];
+            }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < RS; ++j)
 #pragma unroll
             for (int i = 0; i < 2; ++i) asm volatile("" : "+v"(x[j][i]));  // uses stay behind the wait
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < RS; ++j)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if (s0 + j == 0) v[i] = x[j][i];

@@ -96,17 +96,16 @@ int main() {
         printf("  %-40s %8.3f us\n", "round-1 w16_sk RT4 TT2 KB8", time_graph(old, A, W, C, st));
         const int nst = K / 128;
         const int gx = N / 128, gy = (M + 15) / 16;
-        for (int ns : {16, 8, 4}) {
+        for (int ns : {8, 4, 2}) {
             const int ks = (nst + ns - 1) / ns;
             char name[96];
 #define V(R, ABL, TAG)                                                                                            \
             snprintf(name, sizeof name, "w16s R%d %s ns%d ks%d (%d WGs)", R, TAG, ns, ks, gx * gy * ks);          \
             printf("  %-40s %8.3f us\n", name, time_graph(w16s_fn<R, ABL>(M, N, K, ns, ks, ws), A, W, C, st));
             V(2, 0, "full")
-            V(3, 0, "full")
-            V(4, 0, "full")
-            V(3, 1, "DMA only")
-            V(3, 2, "compute only")
+            V(2, 1, "DMA only")
+            V(2, 2, "compute only")
+            V(2, 3, "hand-off only")
 #undef V
             fflush(stdout);
         }
