@@ -53,7 +53,8 @@ typedef enum {
     QG_ALGO_AUTO = 0,
     QG_ALGO_GEMV = 1,    /* M <= 8 (auto: M <= 4): register-resident block decode + v_dot4 */
     QG_ALGO_MFMA = 2,    /* any M (auto: M >= 5), K % 128 == 0: v_mfma_i32_16x16x32_i8 per Q-block */
-    QG_ALGO_GENERIC = 3  /* any K % 32 == 0, any alignment */
+    QG_ALGO_GENERIC = 3, /* any K % 32 == 0, any alignment: byte loads, one wave per output (cross-check) */
+    QG_ALGO_RAGGED = 4   /* any K % 32 == 0 (odd K / 32), 2-B aligned weights: one wave per weight row */
 } qg_algo;
 
 /* ---- W4A8 GEMM, activation-major ---------------------------------------------------------

@@ -96,6 +96,9 @@ int select_algo(const GemmArgs& g) {
     if (g.M <= 4 && gemv_eligible(g)) return QG_ALGO_GEMV;
     if (mfma_eligible(g)) return QG_ALGO_MFMA;
     if (gemv_eligible(g)) return QG_ALGO_GEMV;
+    // odd K / 32 (rows off dword alignment) or 2-B aligned weights: one wave per weight row
+    // (qg_ragged.hip) instead of the byte-load generic kernel's one wave per output
+    if (ragged_eligible(g)) return QG_ALGO_RAGGED;
     return QG_ALGO_GENERIC;
 }
 
@@ -132,9 +135,10 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     // Every item is checked before the first is enqueued (a batch stride can break the MFMA
     // kernel's 16-B alignment for later items only): an explicit MFMA request fails with nothing
     // launched, an automatic choice falls back to the generic kernel for the whole batch.
-    if (algo == QG_ALGO_MFMA) {
+    if (algo == QG_ALGO_MFMA || algo == QG_ALGO_RAGGED) {
+        auto ok = [&](const GemmArgs& gi) { return algo == QG_ALGO_MFMA ? mfma_eligible(gi) : ragged_eligible(gi); };
         bool all_ok = true;
-        for (int i = 0; i < g.batch && all_ok; ++i) all_ok = mfma_eligible(item(i));
+        for (int i = 0; i < g.batch && all_ok; ++i) all_ok = ok(item(i));
         if (!all_ok) {
             if (!auto_algo) return QG_ERR_UNSUPPORTED;
             algo = QG_ALGO_GENERIC;
@@ -146,6 +150,9 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
         switch (algo) {
             case QG_ALGO_MFMA:
                 rc = hip_status(launch_mfma(gi, st));
+                break;
+            case QG_ALGO_RAGGED:
+                rc = hip_status(launch_ragged(gi, st));
                 break;
             case QG_ALGO_GENERIC:
                 rc = hip_status(launch_generic(gi, st));
@@ -439,6 +446,7 @@ int qg_gemm_w4a8_from_view(const qg_tensor_view* act, const qg_tensor_view* w, q
         else if (strcmp(kernel_type, "gemv") == 0) algo = QG_ALGO_GEMV;
         else if (strcmp(kernel_type, "mfma") == 0) algo = QG_ALGO_MFMA;
         else if (strcmp(kernel_type, "generic") == 0) algo = QG_ALGO_GENERIC;
+        else if (strcmp(kernel_type, "ragged") == 0) algo = QG_ALGO_RAGGED;
         else return QG_ERR_INVALID_ARG;
     }
     if (act->type != QG_TYPE_Q8_1 || out->type != QG_TYPE_F32 || !is_weight_type(w->type)) return QG_ERR_UNSUPPORTED;

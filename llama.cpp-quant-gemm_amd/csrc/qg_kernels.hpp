@@ -44,6 +44,11 @@ hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
 // Any shape / alignment with K % 32 == 0 (byte-granular loads); also the debug sumi fallback.
 hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
 
+// Odd K / 32 (weight rows off dword alignment) or 2-B aligned weights: one wave per weight row,
+// realigned dword loads, the GEMV's records and block terms (qg_ragged.hip).
+bool ragged_eligible(const GemmArgs& g);
+hipError_t launch_ragged(const GemmArgs& g, hipStream_t st);
+
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.
 // g.ws / g.ws_bytes: optional caller workspace for the split-K prefill (>= w16_workspace_bytes,
 // 256-B aligned, zero before its first use; left zero by every launch).

@@ -33,7 +33,7 @@ BLOCK_Q8_1_BYTES = 36
 # ggml_type ids (compat/ggml_types.h:199-215)
 Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1 = 2, 3, 6, 7, 8, 9
 BLOCK_BYTES = {Q4_0: 18, Q4_1: 20, Q5_0: 22, Q5_1: 24, Q8_0: 34, Q8_1: 36}
-ALGO_AUTO, ALGO_GEMV, ALGO_MFMA, ALGO_GENERIC = 0, 1, 2, 3
+ALGO_AUTO, ALGO_GEMV, ALGO_MFMA, ALGO_GENERIC, ALGO_RAGGED = 0, 1, 2, 3, 4
 WEIGHT_TYPES = (Q4_0, Q4_1, Q5_0, Q5_1, Q8_0)
 
 

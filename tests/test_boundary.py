@@ -67,8 +67,8 @@ def test_static_queries(lib):
     assert so.qg_select_algo(4, 4096, 4096, 6) == 1      # small batch -> GEMV
     assert so.qg_select_algo(8, 4096, 4096, 6) == 2      # M >= 5 -> MFMA
     assert so.qg_select_algo(32, 4096, 4096, 2) == 2     # prefill -> MFMA
-    assert so.qg_select_algo(1, 4096, 4128, 2) == 3      # K/32 odd -> generic
-    assert so.qg_select_algo(16, 64, 4128, 7) == 3
+    assert so.qg_select_algo(1, 4096, 4128, 2) == 4      # K/32 odd -> one wave per weight row (ragged)
+    assert so.qg_select_algo(16, 64, 4128, 7) == 4
     assert so.qg_select_algo(1, 4096, 33, 2) == -1
     assert so.qg_status_string(-2).decode().startswith("K must be")
     # W4A16 prefill split-K workspace (host-side plan): 512 workgroups of 64 rows x 32 tokens x
@@ -163,7 +163,7 @@ def test_python_mirror_errors_match_reference():
 # configuration query names the kernel qg_gemm_w4a8_ex and qg_debug_sumi would launch.
 PRODUCT_SHAPES = [(1, 4096, 4096), (2, 4096, 4096), (3, 4096, 4096), (4, 4096, 4096), (8, 4096, 4096),
                   (32, 4096, 4096), (1, 4000, 4096), (1, 32000, 4096), (5, 4096, 4096), (128, 4096, 4096),
-                  (512, 4096, 4096), (1, 4096, 14336), (3, 11008, 4096)]
+                  (512, 4096, 4096), (1, 4096, 14336), (3, 11008, 4096), (1, 4096, 4128), (32, 4096, 4128)]
 
 
 @pytest.mark.parametrize("m,n,k", PRODUCT_SHAPES)
@@ -172,7 +172,7 @@ def test_sumi_hook_runs_product_kernel(lib, m, n, k, t):
     import quant_gemm as qg
     prod = qg.debug_config(m, n, k, t)
     assert prod and prod == qg.debug_config(m, n, k, t, sumi=True)
-    fam = {1: "gemv", 2: "mmq", 3: "generic"}[qg.select_algo(m, n, k, t)]
+    fam = {1: "gemv", 2: "mmq", 3: "generic", 4: "ragged"}[qg.select_algo(m, n, k, t)]
     assert prod.startswith(fam + " ")
 
 

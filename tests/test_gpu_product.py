@@ -243,3 +243,46 @@ def test_row_sharded_default_hip_compute(qg, m):
         p.join(timeout=30)
     for rank, ok, err in res:
         assert ok, (rank, err)
+
+
+# Odd K / 32 (every other weight row 2 bytes off dword alignment for Q4_0 / Q5_0 / Q8_0) and 2-B
+# aligned weight tensors: the one-wave-per-weight-row kernel (qg_ragged.hip)
+# instead of the byte-load generic kernel's one wave per output.
+RAGGED = [(1, 4096, 4128), (3, 100, 4128), (9, 64, 1056), (32, 130, 4128), (1, 33, 32), (17, 50, 96), (5, 7, 14368)]
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+@pytest.mark.parametrize("m,n,k", RAGGED)
+def test_ragged_odd_blocks(O, qg, t, m, n, k):
+    """Auto dispatch takes the ragged kernel for odd K/32; int32 sumi bit-exact through the product
+    instantiation, outputs within the summation bound, and the explicit generic kernel agrees."""
+    if (k // 32) % 2 == 1:
+        assert qg.select_algo(m, n, k, t) == 4
+        assert qg.debug_config(m, n, k, t).startswith("ragged ")
+    assert qg.debug_config(m, n, k, t, algo=4) == qg.debug_config(m, n, k, t, algo=4, sumi=True)
+    aq, bq = random_blocks(np.random.default_rng(m * 31 + n + t), m, n, k, t)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t, algo=4))
+    c_ref, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t))
+    tol = O.summation_tol(aq, bq, want, t)
+    assert (np.abs(c.astype(np.float64) - c_ref) <= tol).all()
+    cg = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=3))
+    assert (np.abs(cg.astype(np.float64) - c_ref) <= tol).all()
+
+
+@pytest.mark.parametrize("t", [2, 6, 8])
+def test_ragged_two_byte_aligned_weights(O, qg, t):
+    """A weight tensor starting 2 bytes past a dword (even K/32 too): GEMV / MFMA decline it, the
+    ragged kernel takes it, bit-identical to the same bytes at an aligned address."""
+    import torch
+    m, n, k = 4, 300, 4096
+    aq, bq = random_blocks(np.random.default_rng(t), m, n, k, t)
+    raw = torch.zeros(bq.size + 2, dtype=torch.uint8, device="cuda")
+    raw[2:] = dev(bq.ravel())
+    bmis = raw[2:].view(bq.shape)
+    assert bmis.data_ptr() % 4 == 2
+    c_mis = host(qg.gemm_w4a8(dev(aq), bmis, m, n, k, t))
+    c_rag = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=4))
+    assert np.array_equal(c_mis, c_rag)
+    close_to_oracle(O, c_mis, aq, bq, t)
