@@ -9,10 +9,10 @@
 //  * the workgroup stages its MT activation rows once into LDS records (the GEMV's record,
 //    qg_gemv_kernel.hpp make_act_record: nibble planes for Q4_0 / Q4_1, fp32 d / c*s / -1.5*2^23*d);
 //    record stride 20 dwords (4 x odd: the 16 lanes of a ds_read_b128 group hit distinct bank slots);
-//  * lane l takes blocks l, l + 64, ...: it loads the block's BB bytes as ceil((BB + 2) / 4) dwords
-//    from the dword-aligned address at or below the block (a dword containing a valid byte cannot
-//    cross a page, so the 2 bytes past the last block of a tensor are harmless) and realigns them
-//    with v_alignbyte by the block's 0- or 2-byte offset;
+//  * lane l takes blocks l, l + 64, ...: it loads the dwords covering the block's BB bytes from the
+//    dword-aligned address at or below the block — every loaded dword holds at least one byte of
+//    the block, so none can cross into a page past the tensor — and realigns them with v_alignbyte
+//    by the block's 0- or 2-byte offset;
 //  * the block dot and term are the GEMV's (block_dot / block_term_rec: bit-identical per-block
 //    terms), partials reduced across the wave with DPP (group_sum_last), lane 63 stores.
 #include "qg_gemv_kernel.hpp"
@@ -60,7 +60,12 @@ __global__ __launch_bounds__(RG_WGS) void ragged_kernel(const uint32_t* __restri
         const uint32_t sh = (uint32_t)(pb & 3);  // 0 or 2
         uint32_t d[LD], w[LD];
 #pragma unroll
-        for (int i = 0; i < LD; ++i) d[i] = pa[i];
+        for (int i = 0; i + 1 < LD; ++i) d[i] = pa[i];
+        // the last dword holds block bytes only when the block starts 2 bytes into a dword or its
+        // size is not a dword multiple (Q4_1 / Q5_1 at offset 0 end exactly on a dword boundary: that
+        // dword may lie wholly past the end of the tensor)
+        if constexpr (T::BB % 4 == 0) d[LD - 1] = sh ? pa[LD - 1] : 0u;
+        else d[LD - 1] = pa[LD - 1];
 #pragma unroll
         for (int i = 0; i + 1 < LD; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
         w[LD - 1] = d[LD - 1] >> (8 * sh);

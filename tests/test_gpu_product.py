@@ -271,7 +271,7 @@ def test_ragged_odd_blocks(O, qg, t, m, n, k):
     assert (np.abs(cg.astype(np.float64) - c_ref) <= tol).all()
 
 
-@pytest.mark.parametrize("t", [2, 6, 8])
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
 def test_ragged_two_byte_aligned_weights(O, qg, t):
     """A weight tensor starting 2 bytes past a dword (even K/32 too): GEMV / MFMA decline it, the
     ragged kernel takes it, bit-identical to the same bytes at an aligned address."""
