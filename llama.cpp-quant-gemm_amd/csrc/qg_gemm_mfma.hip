@@ -29,8 +29,19 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
 // us) and the 8-wave 32 x 32 tiles (M = 64 / 96: -0.2 us); the 32 x 16 8-wave tile (M = 32) and
 // the 4-wave tiles keep the general entry (+0.05..+0.55 us with the short one; ab_sig3.txt).
 template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8) || (BN == 32 && TT == 2 && W == 8);
+// Dynamic stage hand-out (MMQ_DYN, qg_mmq_kernel.hpp) for the 32-row x 16-token 8-wave tiles (M <= 32)
+// while the per-stage partial slots fit the LDS (K <= 5120 at 2 KB per 4-block stage).
+#ifndef QG_MMQ_DYN
+#define QG_MMQ_DYN 1
+#endif
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;
+    if constexpr (QG_MMQ_DYN && BN == 32 && TT == 1 && W == 8) {
+        if (mmq_geom<F, BN, TT, W, P16, 2, 4, MMQ_DYN>::dyn_lds(g.K / QK / 4) <= 160 * 1024) {
+            if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true, MMQ_DYN, S>(g, st);
+            return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true, MMQ_DYN, S>(g, st);
+        }
+    }
     if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true, 0, S>(g, st);
     return mmq_launch<F, BN, TT, W, false, P16, 2, 0, false, 4, 1, true, 0, S>(g, st);
 }

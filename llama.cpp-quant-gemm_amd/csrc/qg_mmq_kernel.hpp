@@ -100,7 +100,12 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // K stages (its consecutive stages are adjacent bytes of every row, fetched back to back), instead
 // of stages w, w + W, ...; MMQ_ZL — lanes that must feed zeros into the scale MFMAs (k-slots 1..15)
 // read their scales from a zeroed per-wave LDS region instead of selecting zeros in VALU.
-enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2 };
+// MMQ_DYN — stages handed out dynamically: each wave starts with stages w and w + W, then takes the
+// next unclaimed stage from an LDS counter after every stage it computes, so waves whose DMA lands
+// late take fewer stages (the round-1 timeline had the workgroup's waves finish up to 2 us apart,
+// profiles/r01_tuning/mmq_timeline_r01e.txt). Each stage's partial tile goes to its own LDS slot and
+// the slots are summed in stage order at the end: bit-identical whichever wave took which stage.
+enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4 };
 constexpr int MMQ_ZB = 1024;  // bytes of the per-wave zero region (covers every scale offset)
 
 template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4, int OPT = 0> struct mmq_geom {
@@ -130,6 +135,9 @@ template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4
     static constexpr size_t LDS0 = (size_t)W * (NB * BUF > NACC * 256 ? NB * BUF : NACC * 256);
     static constexpr size_t ZOFF = LDS0;                                   // per-wave zero regions
     static constexpr size_t LDS = LDS0 + ((OPT & MMQ_ZL) ? (size_t)W * MMQ_ZB : 0);
+    // MMQ_DYN: the stage counter (16 B), then one partial tile per stage (dynamic LDS beyond LDS)
+    static constexpr size_t SLOT = (size_t)NACC * 64 * 4;
+    static size_t dyn_lds(int H) { return (OPT & MMQ_DYN) ? LDS + 16 + (size_t)H * SLOT : LDS; }
     static_assert(NB >= 1 && NB <= 4, "1..4 stage buffers per wave");
     static_assert(LDS <= 160 * 1024, "LDS per workgroup");
     static_assert(OFF_A % 16 == 0 && BUF % 16 == 0, "16-B aligned LDS regions");
@@ -534,81 +542,166 @@ const int n0 = blockIdx.x * BN;
         const int h = wave + rot + k * W;
         return h0 + (h >= H ? h - H : h);
     };
-#pragma unroll
-    for (int k = 0; k < NB; ++k)
-        if (k < nst) issue(stage(k), bufs + k * G::BUF);
-    for (int k = 0; k < nst; ++k) {
-        const int h = stage(k);
-        uint8_t* cur = bufs + (k % NB) * G::BUF;
-        wait_stage<G::NI>(min(nst - 1 - k, NB - 1));  // this stage's DMA landed
-#ifdef QG_MMQ_STAMPS
-        if (k == 0) MMQ_STAMP(1);
-#endif
-        if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(cur, h, G::shift(h));
-#ifdef QG_MMQ_STAMPS
-        if (k == 0) MMQ_STAMP(2);
-#endif
-        if (k + NB < nst) issue(stage(k + NB), cur);  // refill the buffer just consumed
-    }
-    MMQ_STAMP(3);
-
-    if constexpr (EPI2 && !SUMI && HAS_S) {
-        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // margin: the last compensation MFMAs (8 needed, header)
-#pragma unroll
-        for (int i = 0; i < G::RT; ++i)
-#pragma unroll
-            for (int t = 0; t < TT; ++t)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[(i * TT + t) * 4 + e] = __builtin_fmaf(CFAC, c2[i][t][e], acc[(i * TT + t) * 4 + e]);
-    }
-    if constexpr (!SUMI) {
-        // fixed-order sum of the W partial tiles, in the wave buffers once every wave is done
-        float* red = reinterpret_cast<float*>(smem);
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < G::NACC; ++i) red[(wave * G::NACC + i) * 64 + lane] = acc[i];
-        __syncthreads();
-        constexpr int TS = G::NACC * 64;  // floats per tile
-        auto wsum = [&](int idx) {
-            float v = red[idx];
-#pragma unroll
-            for (int ww = 1; ww < W; ++ww) v += red[ww * TS + idx];
-            return v;
-        };
-        auto store = [&](int idx, float v) {
-            const int a = idx >> 6, ln = idx & 63;
-            const int e = a & 3, t = (a >> 2) % TT, i = (a >> 2) / TT;
-            const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
-            const int m = m0 + 16 * t + (ln & 15);
-            if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
-        };
-        if constexpr (KS == 1) {
-            for (int idx = threadIdx.x; idx < TS; idx += W * 64) store(idx, wsum(idx));
-        } else {
-            const long tile = (long)blockIdx.y * gridDim.x + blockIdx.x;
-            float* pt = part + tile * KS * TS;
-            // Partials and counter move with agent-scope (sc1) accesses, coherent across the XCDs'
-            // L2s without a release/acquire fence: a fence writes back / invalidates a whole L2,
-            // which other workgroups' cached lines pay for (measured 5-40x slower launches).
-            for (int idx = threadIdx.x; idx < TS; idx += W * 64)
-                __hip_atomic_store(pt + blockIdx.z * TS + idx, wsum(idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is at the coherence point
-            __syncthreads();
-            int* last = reinterpret_cast<int*>(smem);
-            if (threadIdx.x == 0)
-                *last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
-            __syncthreads();
-            if (!*last) return;
-            for (int idx = threadIdx.x; idx < TS; idx += W * 64) {
-                float x[KS];  // every slice's load issued before the first add (atomic loads keep order)
-#pragma unroll
-                for (int s = 0; s < KS; ++s) x[s] = __hip_atomic_load(pt + s * TS + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                float v = x[0];
-#pragma unroll
-                for (int s = 1; s < KS; ++s) v += x[s];
-                store(idx, v);
+    constexpr bool DYN = (OPT & MMQ_DYN) != 0;
+    if constexpr (DYN) {
+        static_assert(NB == 2 && KS == 1 && !CONTIG && !ROT, "dynamic stages: double buffer, no split-K");
+        unsigned* ctr = reinterpret_cast<unsigned*>(smem + G::LDS);
+        uint8_t* slots = smem + G::LDS + 16;
+        if (threadIdx.x == 0) *ctr = 2 * W;  // stages 0 .. 2W - 1 are handed out statically
+        __syncthreads();                     // (no DMA in flight yet)
+        // LDS atomic and slot stores as inline asm: an LDS write the compiler sees makes it wait for
+        // every LDS-DMA in flight (see the header)
+        auto grab = [&]() -> int {
+            unsigned old = 0;
+            if (lane == 0) {
+                const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned*)ctr;
+                asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(a), "v"(1u) : "memory");
             }
-            if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __builtin_amdgcn_readfirstlane((int)old);
+        };
+        auto put = [&](int h) {
+            const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(slots + (size_t)h * G::SLOT) + 16 * lane;
+#pragma unroll
+            for (int j = 0; j < G::NACC / 4; ++j) {
+                const v4i v = {__float_as_int(acc[4 * j]), __float_as_int(acc[4 * j + 1]), __float_as_int(acc[4 * j + 2]),
+                               __float_as_int(acc[4 * j + 3])};
+                asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(j * 1024) : "memory");
+            }
+        };
+        int ha = wave, hb = wave + W;  // stages in buffers A and B (>= H: none)
+        uint8_t* bA = bufs;
+        uint8_t* bB = bufs + G::BUF;
+        if (ha < H) issue(ha, bA);
+        if (hb < H) issue(hb, bB);
+        while (ha < H) {
+            wait_stage<G::NI>(hb < H ? 1 : 0);  // stage ha's DMA landed
+#pragma unroll
+            for (int i = 0; i < G::NACC; ++i) acc[i] = 0.0f;
+            if constexpr (EPI2) {
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) c2[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+            }
+            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(bA, ha, G::shift(ha));
+            if constexpr (!SUMI) {
+                if constexpr (EPI2 && HAS_S) {
+                    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // margin: the stage's compensation MFMAs
+#pragma unroll
+                    for (int i = 0; i < G::RT; ++i)
+#pragma unroll
+                        for (int t = 0; t < TT; ++t)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                acc[(i * TT + t) * 4 + e] = __builtin_fmaf(CFAC, c2[i][t][e], acc[(i * TT + t) * 4 + e]);
+                }
+                put(ha);
+            }
+            const int hn = grab();
+            if (hn < H) issue(hn, bA);  // refill the buffer just consumed
+            ha = hb;
+            hb = hn;
+            uint8_t* t = bA;
+            bA = bB;
+            bB = t;
+        }
+        MMQ_STAMP(3);
+        if constexpr (!SUMI) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slot stores
+            __syncthreads();
+            constexpr int TS = G::NACC * 64;
+            for (int c = threadIdx.x; c < TS / 4; c += W * 64) {  // 16-B chunk c = (j, ln): acc 4j..4j+3 of lane ln
+                const float* p = reinterpret_cast<const float*>(slots) + 4 * c;
+                f32x4v v = *reinterpret_cast<const f32x4v*>(p);
+                for (int h = 1; h < H; ++h) v += *reinterpret_cast<const f32x4v*>(p + (size_t)h * TS);
+                const int j = c >> 6, ln = c & 63;
+#pragma unroll
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    const int a = 4 * j + e4;
+                    const int e = a & 3, t = (a >> 2) % TT, i = (a >> 2) / TT;
+                    const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
+                    const int m = m0 + 16 * t + (ln & 15);
+                    if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v[e4];
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+            if (k < nst) issue(stage(k), bufs + k * G::BUF);
+        for (int k = 0; k < nst; ++k) {
+            const int h = stage(k);
+            uint8_t* cur = bufs + (k % NB) * G::BUF;
+            wait_stage<G::NI>(min(nst - 1 - k, NB - 1));  // this stage's DMA landed
+    #ifdef QG_MMQ_STAMPS
+            if (k == 0) MMQ_STAMP(1);
+    #endif
+            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(cur, h, G::shift(h));
+    #ifdef QG_MMQ_STAMPS
+            if (k == 0) MMQ_STAMP(2);
+    #endif
+            if (k + NB < nst) issue(stage(k + NB), cur);  // refill the buffer just consumed
+        }
+        MMQ_STAMP(3);
+    
+        if constexpr (EPI2 && !SUMI && HAS_S) {
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // margin: the last compensation MFMAs (8 needed, header)
+    #pragma unroll
+            for (int i = 0; i < G::RT; ++i)
+    #pragma unroll
+                for (int t = 0; t < TT; ++t)
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[(i * TT + t) * 4 + e] = __builtin_fmaf(CFAC, c2[i][t][e], acc[(i * TT + t) * 4 + e]);
+        }
+        if constexpr (!SUMI) {
+            // fixed-order sum of the W partial tiles, in the wave buffers once every wave is done
+            float* red = reinterpret_cast<float*>(smem);
+            __syncthreads();
+    #pragma unroll
+            for (int i = 0; i < G::NACC; ++i) red[(wave * G::NACC + i) * 64 + lane] = acc[i];
+            __syncthreads();
+            constexpr int TS = G::NACC * 64;  // floats per tile
+            auto wsum = [&](int idx) {
+                float v = red[idx];
+    #pragma unroll
+                for (int ww = 1; ww < W; ++ww) v += red[ww * TS + idx];
+                return v;
+            };
+            auto store = [&](int idx, float v) {
+                const int a = idx >> 6, ln = idx & 63;
+                const int e = a & 3, t = (a >> 2) % TT, i = (a >> 2) / TT;
+                const int n = n0 + 16 * i + 4 * (ln >> 4) + e;
+                const int m = m0 + 16 * t + (ln & 15);
+                if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v;
+            };
+            if constexpr (KS == 1) {
+                for (int idx = threadIdx.x; idx < TS; idx += W * 64) store(idx, wsum(idx));
+            } else {
+                const long tile = (long)blockIdx.y * gridDim.x + blockIdx.x;
+                float* pt = part + tile * KS * TS;
+                // Partials and counter move with agent-scope (sc1) accesses, coherent across the XCDs'
+                // L2s without a release/acquire fence: a fence writes back / invalidates a whole L2,
+                // which other workgroups' cached lines pay for (measured 5-40x slower launches).
+                for (int idx = threadIdx.x; idx < TS; idx += W * 64)
+                    __hip_atomic_store(pt + blockIdx.z * TS + idx, wsum(idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is at the coherence point
+                __syncthreads();
+                int* last = reinterpret_cast<int*>(smem);
+                if (threadIdx.x == 0)
+                    *last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+                __syncthreads();
+                if (!*last) return;
+                for (int idx = threadIdx.x; idx < TS; idx += W * 64) {
+                    float x[KS];  // every slice's load issued before the first add (atomic loads keep order)
+    #pragma unroll
+                    for (int s = 0; s < KS; ++s) x[s] = __hip_atomic_load(pt + s * TS + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    float v = x[0];
+    #pragma unroll
+                    for (int s = 1; s < KS; ++s) v += x[s];
+                    store(idx, v);
+                }
+                if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 #ifdef QG_MMQ_STAMPS
@@ -693,16 +786,17 @@ hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
     }
     if constexpr (SHORT && KS == 1 && ABL == 0 && !ROT) {  // (mmq_shape_ok: 32-bit output strides)
         auto k1 = mmq1_kernel<F, BN, TT, W, SUMI, P16, NB, SB, EPI2, OPT>;
-        if (G::LDS > 64 * 1024) {
+        const size_t lds = G::dyn_lds(g.K / QK / SB);
+        if (lds > 64 * 1024) {
             static bool attr1_set = false;  // once per instantiation (not a stream op: capture-safe)
             if (!attr1_set) {
-                hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+                hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (e != hipSuccess) return e;
                 attr1_set = true;
             }
         }
         void* out = SUMI ? (void*)g.sumi : (void*)g.C;
-        hipLaunchKernelGGL(k1, grid, dim3(W * 64), G::LDS, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.M, g.N, g.K, out,
+        hipLaunchKernelGGL(k1, grid, dim3(W * 64), lds, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.M, g.N, g.K, out,
                            (int)g.ldc_m, (int)g.ldc_n);
         return hipGetLastError();
     } else {
@@ -716,15 +810,16 @@ hipError_t mmq_launch_full(const GemmArgs& g, hipStream_t st, dim3 grid) {
     auto k = mmq_kernel<F, BN, TT, W, SUMI, P16, NB, ABL, ROT, SB, KS, EPI2, OPT>;
     unsigned* cnt = KS > 1 ? (unsigned*)g.ws : nullptr;
     float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
-    if (G::LDS > 64 * 1024) {
+    const size_t lds = G::dyn_lds(g.K / QK / SB / KS);
+    if (lds > 64 * 1024) {
         static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
         if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
     }
-    hipLaunchKernelGGL(k, grid, dim3(W * 64), G::LDS, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.C, g.sumi, g.M,
+    hipLaunchKernelGGL(k, grid, dim3(W * 64), lds, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.C, g.sumi, g.M,
                        g.N, g.K, g.ldc_m, g.ldc_n, part, cnt);
     return hipGetLastError();
 }
