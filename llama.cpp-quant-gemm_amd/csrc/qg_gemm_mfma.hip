@@ -29,10 +29,12 @@ template <int F, int BN, int TT, int W> bool ok_cfg(const GemmArgs& g) {
 // us) and the 8-wave 32 x 32 tiles (M = 64 / 96: -0.2 us); the 32 x 16 8-wave tile (M = 32) and
 // the 4-wave tiles keep the general entry (+0.05..+0.55 us with the short one; ab_sig3.txt).
 template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8) || (BN == 32 && TT == 2 && W == 8);
-// Dynamic stage hand-out (MMQ_DYN, qg_mmq_kernel.hpp) for the 32-row x 16-token 8-wave tiles (M <= 32)
-// while the per-stage partial slots fit the LDS (K <= 5120 at 2 KB per 4-block stage).
+// Dynamic stage hand-out (MMQ_DYN, qg_mmq_kernel.hpp) for the 32-row x 16-token 8-wave tiles: a
+// tuning option, off in the product — measured slower (profiles/r02_tuning/ab_dyn.txt: M=32 6.87 ->
+// 7.25 us, N=11008 14.6 -> 18.8 us: the per-stage partial slots take the LDS to 144 KB, one
+// workgroup per CU, and the stage-order sum adds a tail; the waves' spread is not intra-workgroup).
 #ifndef QG_MMQ_DYN
-#define QG_MMQ_DYN 1
+#define QG_MMQ_DYN 0
 #endif
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;

@@ -105,6 +105,7 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // late take fewer stages (the round-1 timeline had the workgroup's waves finish up to 2 us apart,
 // profiles/r01_tuning/mmq_timeline_r01e.txt). Each stage's partial tile goes to its own LDS slot and
 // the slots are summed in stage order at the end: bit-identical whichever wave took which stage.
+// A tuning option (QG_MMQ_DYN, qg_gemm_mfma.hip): measured slower, off in the product.
 enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4 };
 constexpr int MMQ_ZB = 1024;  // bytes of the per-wave zero region (covers every scale offset)
 
