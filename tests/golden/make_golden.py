@@ -92,6 +92,10 @@ def main() -> None:
     cases["w4a8_q4_0_m8n4k4096"] = w4a8_case(run_q4_0, 8, 4, 4096, O.Q4_0)
     cases["w4a8_q4_1_m1n4k4096"] = w4a8_case(run_q4_1, 1, 4, 4096, O.Q4_1)
     cases["w4a16_q4_0_m1n4k4096"] = w4a16_case(run_w4a16, 1, 4, 4096)
+    # odd K / 32 (129 blocks: every other weight row 2 bytes off dword alignment) — the ragged kernel
+    # on the GPU (QG_ALGO_RAGGED, round 2)
+    cases["w4a8_q4_0_m3n8k4128"] = w4a8_case(run_q4_0, 3, 8, 4128, O.Q4_0, seed=11)
+    cases["w4a8_q4_1_m2n8k4128"] = w4a8_case(run_q4_1, 2, 8, 4128, O.Q4_1, seed=13)
     for name, d in cases.items():
         path = os.path.join(HERE, f"{name}.npz")
         if os.path.exists(path) and not args.force:
