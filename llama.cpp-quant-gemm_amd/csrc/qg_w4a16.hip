@@ -640,42 +640,43 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
 // The K slices of a tile meet through the workspace: 16-B write-through (sc1) partial stores, a
 // per-tile agent-scope counter, and the last slice to arrive sums the partials in slice order
 // (deterministic) with sc1 loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1).
-namespace w16s {
-constexpr int ROWS = 128;              // weight rows per workgroup (4 waves x 2 tiles of 16)
-constexpr int TOK = 16;                // tokens per workgroup
-constexpr int RSB = 4 * 18;            // Q4_0 bytes per row per stage (4 blocks)
-constexpr int RIMG = RSB + 8;          // 16-B aligned row window (80 B)
-constexpr int PPR = RIMG / 16;         // 16-B pieces per row window
-constexpr int WP = ROWS * PPR;         // weight pieces per stage (640)
-constexpr int ATS = 33;                // pieces per token image (32 data + 1 pad)
-constexpr int AP = TOK * ATS;          // activation pieces per stage (528)
-constexpr int NI = 20;                 // DMA instructions per stage: ceil(1168 / 64) = 19, padded to 4 waves
-constexpr int NIW = NI / 4;            // per wave
-constexpr int SBYTES = NI * 1024;      // LDS bytes per stage
-constexpr int AOFF = WP * 16;          // activation image offset in a stage
-constexpr int PT = 4 * 2 * 64 * 4;     // floats per partial tile (4 waves x 2 tiles x 64 lanes x 4)
-constexpr int PLB = 3 * 4 * 1024;      // activation planes of one stage (bf16 hi / mid / lo operand fragments)
-static_assert(WP + AP <= NI * 64, "stage pieces fit the DMA instructions");
-}  // namespace w16s
+// TT: 16-token tiles per workgroup (1: 16 tokens; 2: 32 tokens, each weight fragment decoded once
+// for both token tiles).
+template <int TT> struct w16s_geom {
+    static constexpr int ROWS = 128;              // weight rows per workgroup (4 waves x 2 tiles of 16)
+    static constexpr int TOK = 16 * TT;           // tokens per workgroup
+    static constexpr int RSB = 4 * 18;            // Q4_0 bytes per row per stage (4 blocks)
+    static constexpr int RIMG = RSB + 8;          // 16-B aligned row window (80 B)
+    static constexpr int PPR = RIMG / 16;         // 16-B pieces per row window
+    static constexpr int WP = ROWS * PPR;         // weight pieces per stage (640)
+    static constexpr int ATS = 33;                // pieces per token image (32 data + 1 pad)
+    static constexpr int AP = TOK * ATS;          // activation pieces per stage
+    static constexpr int NI = ((WP + AP + 63) / 64 + 3) / 4 * 4;  // DMA instructions per stage (whole per wave)
+    static constexpr int NIW = NI / 4;            // per wave
+    static constexpr int SBYTES = NI * 1024;      // LDS bytes per stage
+    static constexpr int AOFF = WP * 16;          // activation image offset in a stage
+    static constexpr int PT = 4 * 2 * TT * 64 * 4;  // floats per partial tile (4 waves x 2 x TT tiles x 64 lanes x 4)
+    static constexpr int PLB = 3 * 4 * TT * 1024;   // activation planes of one stage ([plane][block][tt][lane] x 16 B)
+    static_assert(WP + AP <= NI * 64, "stage pieces fit the DMA instructions");
+};
 
 __device__ __forceinline__ void w16_glds16(const uint8_t* g, uint8_t* l) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 // s_waitcnt vmcnt(k * NIW): this wave's DMA of the oldest stage in flight landed, k later ones may fly
-__device__ __forceinline__ void w16s_wait(int k) {
+template <int NIW> __device__ __forceinline__ void w16s_wait(int k) {
     switch (k) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIW) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIW) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NIW) : "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NIW) : "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * NIW) : "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * NIW) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * NIW) : "memory"); break;
     }
 }
-static_assert(w16s::NIW == 5, "w16s_wait counts 5 DMA instructions per wave and stage");
 
 // 16-B write-through store / L2-served load (the hand-off's sc1 accesses)
 __device__ __forceinline__ void st_x4_sc1(float* p, f32x4_t v) {
@@ -717,53 +718,60 @@ __device__ __forceinline__ void ds_write_x4_asm(uint8_t* p, u32x4_t v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 
-// The activation planes of one stage, split once per workgroup: wave w takes block w of the stage;
-// lane (r16, q) reads its token's 8 fp32 of k-slot q (elements 4q.. and 16+4q.., two 16-B pieces of
-// the raw image) and writes a = hi + mid + lo (truncated bf16 parts, exact) as three 16-B operand
-// fragments, planes [plane][block][lane] (1 KiB each: conflict-free ds_read_b128 / write).
+// The activation planes of one stage, split once per workgroup: wave w takes block w of the stage
+// (for every token tile); lane (r16, q) reads its token's 8 fp32 of k-slot q (elements 4q.. and
+// 16+4q.., two 16-B pieces of the raw image) and writes a = hi + mid + lo (truncated bf16 parts,
+// exact) as three 16-B operand fragments, planes [plane][block][tt][lane] (1 KiB each).
+template <int TT>
 __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, int wave, int lane) {
-    using namespace w16s;
+    using G = w16s_geom<TT>;
     const int r16 = lane & 15, q = lane >> 4;
-    const uint8_t* ar = sb + AOFF + r16 * (ATS * 16) + 128 * wave;
-    const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(ar + 16 * q);
-    const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(ar + 64 + 16 * q);
-    const float a[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    uint32_t r1[8], r2[8];
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-        const f32x2 x = {a[j], a[j + 1]};
-        const f32x2 h = {__uint_as_float(__float_as_uint(a[j]) & 0xFFFF0000u), __uint_as_float(__float_as_uint(a[j + 1]) & 0xFFFF0000u)};
-        const f32x2 m1 = x - h;  // exact
-        const f32x2 mh = {__uint_as_float(__float_as_uint(m1.x) & 0xFFFF0000u), __uint_as_float(__float_as_uint(m1.y) & 0xFFFF0000u)};
-        const f32x2 l2 = m1 - mh;  // exact, <= 8 significant bits
-        r1[j] = __float_as_uint(m1.x); r1[j + 1] = __float_as_uint(m1.y);
-        r2[j] = __float_as_uint(l2.x); r2[j + 1] = __float_as_uint(l2.y);
-    }
-    u32x4_t ph, pm, pl;
+    for (int t = 0; t < TT; ++t) {
+        const uint8_t* ar = sb + G::AOFF + (16 * t + r16) * (G::ATS * 16) + 128 * wave;
+        const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(ar + 16 * q);
+        const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(ar + 64 + 16 * q);
+        const float a[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        uint32_t r1[8], r2[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        ph[k] = hi16_pack(__float_as_uint(a[2 * k]), __float_as_uint(a[2 * k + 1]));
-        pm[k] = hi16_pack(r1[2 * k], r1[2 * k + 1]);
-        pl[k] = hi16_pack(r2[2 * k], r2[2 * k + 1]);
+        for (int j = 0; j < 8; j += 2) {
+            const f32x2 x = {a[j], a[j + 1]};
+            const f32x2 h = {__uint_as_float(__float_as_uint(a[j]) & 0xFFFF0000u), __uint_as_float(__float_as_uint(a[j + 1]) & 0xFFFF0000u)};
+            const f32x2 m1 = x - h;  // exact
+            const f32x2 mh = {__uint_as_float(__float_as_uint(m1.x) & 0xFFFF0000u), __uint_as_float(__float_as_uint(m1.y) & 0xFFFF0000u)};
+            const f32x2 l2 = m1 - mh;  // exact, <= 8 significant bits
+            r1[j] = __float_as_uint(m1.x); r1[j + 1] = __float_as_uint(m1.y);
+            r2[j] = __float_as_uint(l2.x); r2[j + 1] = __float_as_uint(l2.y);
+        }
+        u32x4_t ph, pm, pl;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ph[k] = hi16_pack(__float_as_uint(a[2 * k]), __float_as_uint(a[2 * k + 1]));
+            pm[k] = hi16_pack(r1[2 * k], r1[2 * k + 1]);
+            pl[k] = hi16_pack(r2[2 * k], r2[2 * k + 1]);
+        }
+        uint8_t* d = planes + (size_t)(wave * TT + t) * 1024 + 16 * lane;
+        ds_write_x4_asm(d, ph);
+        ds_write_x4_asm(d + 4 * TT * 1024, pm);
+        ds_write_x4_asm(d + 8 * TT * 1024, pl);
     }
-    uint8_t* d = planes + (size_t)wave * 1024 + 16 * lane;
-    ds_write_x4_asm(d, ph);
-    ds_write_x4_asm(d + 4 * 1024, pm);
-    ds_write_x4_asm(d + 8 * 1024, pl);
 }
 
 // One 4-block stage of a wave (SH: the data's byte offset in the row windows, 0 on even stages, 8
-// on odd ones). acc[i][e]: token 4q + e, weight row 32 wave + 16 i + r16.
-template <int SH>
+// on odd ones). acc[i][t][e]: token 16 t + 4q + e, weight row 32 wave + 16 i + r16.
+template <int TT, int SH>
 __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* planes, int wave, int lane,
-                                           f32x4_t (&acc)[2]) {
-    using namespace w16s;
+                                           f32x4_t (&acc)[2][TT]) {
+    using G = w16s_geom<TT>;
     const int r16 = lane & 15, q = lane >> 4;
-    u32x4_t ap[3][4];
+    u32x4_t ap[3][4][TT];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) ap[pl][b] = *reinterpret_cast<const u32x4_t*>(planes + (pl * 4 + b) * 1024 + 16 * lane);
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                ap[pl][b][t] = *reinterpret_cast<const u32x4_t*>(planes + ((pl * 4 + b) * TT + t) * 1024 + 16 * lane);
     u32x4_t wf[4][2];
     float dw[4][2];
     static_for<4>([&](auto BI) {
@@ -773,7 +781,7 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
         constexpr int D = SH + 18 * b;       // its f16 d
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const uint8_t* row = sb + (32 * wave + 16 * i + r16) * RIMG;
+            const uint8_t* row = sb + (32 * wave + 16 * i + r16) * G::RIMG;
             const uint32_t* pw = reinterpret_cast<const uint32_t*>(row + (X0 & ~3) + 4 * q);
             uint32_t v = pw[0];
             if constexpr (al != 0) v = __builtin_amdgcn_alignbyte(pw[1], v, al);
@@ -782,21 +790,26 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
         }
     });
     __builtin_amdgcn_sched_barrier(0);
-    f32x4_t c[4][2];
+    f32x4_t c[4][2][TT];
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0][b]), __builtin_bit_cast(bf16x8_t, wf[b][i]),
-                                                              f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                c[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0][b][t]),
+                                                                     __builtin_bit_cast(bf16x8_t, wf[b][i]),
+                                                                     f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
     for (int pl = 1; pl < 3; ++pl)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl][b]),
-                                                                  __builtin_bit_cast(bf16x8_t, wf[b][i]), c[b][i], 0, 0, 0);
+#pragma unroll
+                for (int t = 0; t < TT; ++t)
+                    c[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl][b][t]),
+                                                                         __builtin_bit_cast(bf16x8_t, wf[b][i]), c[b][i][t], 0, 0, 0);
     // MFMA results read by the VALU behind an explicit wait (8 states needed; qg_mmq_kernel.hpp)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -806,99 +819,109 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][e] = __builtin_fmaf(dw[b][i], c[b][i][e], acc[i][e]);
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][t][e] = __builtin_fmaf(dw[b][i], c[b][i][t][e], acc[i][t][e]);
 }
 
-// grid (ceil(N / 128), ceil(M / 16), ks); slice z = stages [z * ns, min(nst, (z + 1) * ns)) of the
-// nst = K / 128 stages. ks == 1: direct stores, no workspace.
-// R: LDS stage slots (0: every stage of the slice its own slot, all put in flight at kernel start;
-// R >= 2: a ring of R slots, R - 1 stages in flight ahead of the one being computed, a slot refilled
+// grid (ceil(N / 128), ceil(M / (16 TT)), ks); slice z = stages [z * ns, min(nst, (z + 1) * ns)) of
+// the nst = K / 128 stages. ks == 1: direct stores, no workspace.
+// R: LDS stage slots (a ring, R - 1 stages in flight ahead of the one being computed, a slot refilled
 // right after the barrier that follows its last reader). After the raw activation planes of stage s
 // have landed, the workgroup splits them once (w16s_split) into the planes buffer, a second barrier
 // publishes it, and every wave computes the stage. ABL (tuning probes only): 1 = DMA and waits
 // without split / compute, 2 = split + compute on whatever the LDS holds, no DMA, 3 = neither (the
 // launch, barriers and the split-K hand-off alone).
-template <int R, int ABL>
+template <int TT, int R, int ABL>
 __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int M, int N, int K, long ldc_m, long ldc_n,
                                                    int ns, float* __restrict__ part, unsigned* __restrict__ cnt) {
-    using namespace w16s;
+    using G = w16s_geom<TT>;
     static_assert(R >= 2 && R <= 7, "ring slots (w16s_wait counts up to 7 younger stages)");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int n0 = blockIdx.x * ROWS, m0 = blockIdx.y * TOK;
+    const int n0 = blockIdx.x * G::ROWS, m0 = blockIdx.y * G::TOK;
     const int nst = K / 128;
     const int h0 = blockIdx.z * ns;
     const int nloc = min(ns, nst - h0);  // stages of this slice
     const long RB = (long)(K / QK) * 18;
-    uint8_t* planes = lds + R * SBYTES;  // 12 KiB: [plane][block][lane] x 16 B
+    uint8_t* planes = lds + R * G::SBYTES;
 
     // this wave's DMA instructions i = wave + 4 k: piece p = 64 i + lane (clamped into the padding)
-    const uint8_t* src[NIW];
-    bool isw[NIW];
+    const uint8_t* src[G::NIW];
+    bool isw[G::NIW];
 #pragma unroll
-    for (int k = 0; k < NIW; ++k) {
-        const int p = min(64 * (wave + 4 * k) + lane, WP + AP - 1);
-        isw[k] = p < WP;
+    for (int k = 0; k < G::NIW; ++k) {
+        const int p = min(64 * (wave + 4 * k) + lane, G::WP + G::AP - 1);
+        isw[k] = p < G::WP;
         if (isw[k]) {
-            const int row = p / PPR, j = p - (p / PPR) * PPR;
+            const int row = p / G::PPR, j = p - (p / G::PPR) * G::PPR;
             src[k] = B + (long)min(n0 + row, N - 1) * RB + 16 * j;
         } else {
-            const int a = p - WP, tok = a / ATS, j = min(a - (a / ATS) * ATS, 31);
+            const int a = p - G::WP, tok = a / G::ATS, j = min(a - (a / G::ATS) * G::ATS, 31);
             src[k] = reinterpret_cast<const uint8_t*>(A + (long)min(m0 + tok, M - 1) * K) + 16 * j;
         }
     }
-    auto slot = [&](int s) { return lds + (s % R) * SBYTES; };
+    auto slot = [&](int s) { return lds + (s % R) * G::SBYTES; };
     auto issue = [&](int s) {
         if constexpr (ABL >= 2) return;
         const int h = h0 + s;
-        const long dw = (long)h * RSB - ((h & 1) ? 8 : 0), da = (long)h * 512;
+        const long dw = (long)h * G::RSB - ((h & 1) ? 8 : 0), da = (long)h * 512;
         uint8_t* dst = slot(s) + 1024 * wave;
 #pragma unroll
-        for (int k = 0; k < NIW; ++k) w16_glds16(src[k] + (isw[k] ? dw : da), dst + 4096 * k);
+        for (int k = 0; k < G::NIW; ++k) w16_glds16(src[k] + (isw[k] ? dw : da), dst + 4096 * k);
     };
     constexpr int AHEAD = R - 1;  // stages in flight ahead of the one being computed
     for (int s = 0; s < min(nloc, AHEAD); ++s) issue(s);
 
-    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+    f32x4_t acc[2][TT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[i][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < nloc; ++s) {
         // stages issued so far: 0 .. min(nloc, s + AHEAD) - 1; wait for stage s
-        if constexpr (ABL < 2) w16s_wait(min(nloc, s + AHEAD) - 1 - s);
+        if constexpr (ABL < 2) w16s_wait<G::NIW>(min(nloc, s + AHEAD) - 1 - s);
         __builtin_amdgcn_s_barrier();  // stage s landed everywhere; stage s - 1 and the planes are free
         asm volatile("" ::: "memory");
         if (s + AHEAD < nloc) issue(s + AHEAD);  // into the slot of stage s - 1
         if constexpr (ABL != 1 && ABL != 3) {
-            w16s_split(slot(s), planes, wave, lane);
+            w16s_split<TT>(slot(s), planes, wave, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // planes of stage s published
             asm volatile("" ::: "memory");
-            if ((h0 + s) & 1) w16s_stage<8>(slot(s), planes, wave, lane, acc);
-            else w16s_stage<0>(slot(s), planes, wave, lane, acc);
+            if ((h0 + s) & 1) w16s_stage<TT, 8>(slot(s), planes, wave, lane, acc);
+            else w16s_stage<TT, 0>(slot(s), planes, wave, lane, acc);
         }
     }
 
-    // lane: weight rows n0 + 32 wave + 16 i + r16, tokens m0 + 4 q + e
+    // lane: weight rows n0 + 32 wave + 16 i + r16, tokens m0 + 16 t + 4 q + e
     const int r16 = lane & 15, q = lane >> 4;
-    auto store = [&](int i, const f32x4_t& v) {
+    auto store = [&](int i, int t, const f32x4_t& v) {
         const int n = n0 + 32 * wave + 16 * i + r16;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int m = m0 + 4 * q + e;
+            const int m = m0 + 16 * t + 4 * q + e;
             if (n < N && m < M) C[m * ldc_m + n * ldc_n] = v[e];
         }
     };
     if (gridDim.z == 1) {
-        store(0, acc[0]);
-        store(1, acc[1]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < TT; ++t) store(i, t, acc[i][t]);
         return;
     }
     const int KS = gridDim.z;
     const long tile = (long)blockIdx.y * gridDim.x + blockIdx.x;
-    float* pt = part + tile * KS * PT;
-    auto pidx = [&](int i) { return ((wave * 2 + i) * 64 + lane) * 4; };  // 16 B per lane, whole lines per wave
-    st_x4_sc1(pt + blockIdx.z * PT + pidx(0), acc[0]);
-    st_x4_sc1(pt + blockIdx.z * PT + pidx(1), acc[1]);
+    float* pt = part + tile * KS * G::PT;
+    // 16 B per lane, whole lines per wave instruction
+    auto pidx = [&](int i, int t) { return (((wave * 2 + i) * TT + t) * 64 + lane) * 4; };
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) st_x4_sc1(pt + blockIdx.z * G::PT + pidx(i, t), acc[i][t]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's partial is at the coherence point
     __syncthreads();
     int* last = reinterpret_cast<int*>(lds);
@@ -906,36 +929,46 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
         *last = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)KS - 1;
     __syncthreads();
     if (!*last) return;
-    // slice-order sum, up to 8 slices' loads in flight per round; this slice's own partial from registers
-    constexpr int RS = 8;
+    // slice-order sum, up to RS slices' loads in flight per round; this slice's own partial from registers
+    constexpr int RS = TT == 1 ? 8 : 4;
     const int z = blockIdx.z;
-    f32x4_t v[2];
+    f32x4_t v[2][TT];
     for (int s0 = 0; s0 < KS; s0 += RS) {
-        f32x4_t x[RS][2];
+        f32x4_t x[RS][2][TT];
 #pragma unroll
         for (int j = 0; j < RS; ++j)
             if (s0 + j < KS && s0 + j != z) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) x[j][i] = ld_x4_sc1(pt + (s0 + j) * PT + pidx(i));
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) x[j][i][t] = ld_x4_sc1(pt + (s0 + j) * G::PT + pidx(i, t));
             } else {
-                x[j][0] = acc[0];
-                x[j][1] = acc[1];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) x[j][i][t] = acc[i][t];
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < RS; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) asm volatile("" : "+v"(x[j][i]));  // uses stay behind the wait
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) asm volatile("" : "+v"(x[j][i][t]));  // uses stay behind the wait
 #pragma unroll
         for (int j = 0; j < RS; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (s0 + j == 0) v[i] = x[j][i];
-                else if (s0 + j < KS) v[i] += x[j][i];
-            }
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    if (s0 + j == 0) v[i][t] = x[j][i][t];
+                    else if (s0 + j < KS) v[i][t] += x[j][i][t];
+                }
     }
-    store(0, v[0]);
-    store(1, v[1]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) store(i, t, v[i][t]);
     if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1060,11 +1093,15 @@ w16_plan w16_make_plan(int M, int N, int K) {
 #ifndef W16S_R
 #define W16S_R 2  // LDS ring slots of w16s_kernel (2: one stage in flight ahead; 3-4 measured slower)
 #endif
+#ifndef W16S_TT2
+#define W16S_TT2 0  // 32-token tiles for M > 16 (tuning knob)
+#endif
 w16_plan w16s_make_plan(int M, int N, int K) {
     w16_plan p;
     if (!QG_W16S || M <= 8 || M > 64 || N < 1 || K % 256 != 0) return p;
-    p.gx = (N + w16s::ROWS - 1) / w16s::ROWS;
-    p.gy = (M + w16s::TOK - 1) / w16s::TOK;
+    p.tt = W16S_TT2 && M > 16 ? 2 : 1;
+    p.gx = (N + 127) / 128;
+    p.gy = (M + 16 * p.tt - 1) / (16 * p.tt);
     const long tiles = p.gx * p.gy;
     const int nst = K / 128;
     // >= 512 workgroups (two per CU overlap each other's barriers and LDS latency) with >= 4 stages per
@@ -1074,24 +1111,29 @@ w16_plan w16s_make_plan(int M, int N, int K) {
     p.ns = (nst + ks - 1) / ks;
     p.ks = (nst + p.ns - 1) / p.ns;
     if (p.ks > 1 && tiles > (long)(W16_CNT_BYTES / 4)) return w16_plan{};
-    if (p.ks > 1) p.ws_bytes = W16_CNT_BYTES + (size_t)tiles * p.ks * w16s::PT * 4;
+    const size_t pt = p.tt == 2 ? w16s_geom<2>::PT : w16s_geom<1>::PT;
+    if (p.ks > 1) p.ws_bytes = W16_CNT_BYTES + (size_t)tiles * p.ks * pt * 4;
     return p;
 }
 
-hipError_t w16s_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+template <int TT> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    using G = w16s_geom<TT>;
     unsigned* cnt = (unsigned*)ws;
     float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
-    const size_t lds = (size_t)W16S_R * w16s::SBYTES + w16s::PLB;
-    static bool attr_set = false;  // once (not a stream op: capture-safe)
+    constexpr size_t lds = (size_t)W16S_R * G::SBYTES + G::PLB;
+    static_assert(lds <= 160 * 1024, "LDS per workgroup");
+    static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)w16s_kernel<W16S_R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(W16S_R * w16s::SBYTES + w16s::PLB));
+        hipError_t e = hipFuncSetAttribute((const void*)w16s_kernel<TT, W16S_R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((w16s_kernel<W16S_R, 0>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A, (const uint8_t*)g.B,
-                       g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n, p.ns, part, cnt);
+    hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
+                       (const uint8_t*)g.B, g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n, p.ns, part, cnt);
     return hipGetLastError();
+}
+hipError_t w16s_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    return p.tt == 2 ? w16s_launch_tt<2>(g, p, ws, st) : w16s_launch_tt<1>(g, p, ws, st);
 }
 
 template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs& g, const w16_plan& p, void* ws,

@@ -48,13 +48,13 @@ static double time_graph(const Fn& fn, const float* A, std::vector<uint8_t*>& W,
     return v[2];
 }
 
-template <int R, int ABL> Fn w16s_fn(int M, int N, int K, int ns, int ks, void* ws) {
+template <int TT, int R, int ABL> Fn w16s_fn(int M, int N, int K, int ns, int ks, void* ws) {
     return [=](const float* A, const uint8_t* B, float* C, hipStream_t st) {
-        auto k = w16s_kernel<R, ABL>;
+        auto k = w16s_kernel<TT, R, ABL>;
         static bool set = false;
-        const size_t lds = (size_t)R * w16s::SBYTES + w16s::PLB;
+        const size_t lds = (size_t)R * w16s_geom<TT>::SBYTES + w16s_geom<TT>::PLB;
         if (!set) { CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); set = true; }
-        const int gx = (N + 127) / 128, gy = (M + 15) / 16;
+        const int gx = (N + 127) / 128, gy = (M + 16 * TT - 1) / (16 * TT);
         hipLaunchKernelGGL(k, dim3(gx, gy, ks), dim3(256), lds, st, A, B, C, M, N, K, (long)N, 1L, ns,
                            (float*)((uint8_t*)ws + 4096), (unsigned*)ws);
     };
@@ -81,7 +81,7 @@ int main() {
     hipStream_t st;
     CK(hipStreamCreate(&st));
     struct S { int M, K; };
-    for (S s : {S{32, 4096}, S{16, 4096}, S{64, 4096}}) {
+    for (S s : {S{32, 4096}, S{64, 4096}, S{24, 4096}}) {
         const int M = s.M, K = s.K;
         const size_t wb = (size_t)N * (K / 32) * 18;
         for (auto& p : W) { CK(hipMalloc(&p, wb)); CK(hipMemcpy(p, h.data(), wb, hipMemcpyHostToDevice)); }
@@ -95,17 +95,20 @@ int main() {
         };
         printf("  %-40s %8.3f us\n", "round-1 w16_sk RT4 TT2 KB8", time_graph(old, A, W, C, st));
         const int nst = K / 128;
-        const int gx = N / 128, gy = (M + 15) / 16;
+        const int gx = N / 128;
         for (int ns : {8, 4, 2}) {
             const int ks = (nst + ns - 1) / ns;
             char name[96];
-#define V(R, ABL, TAG)                                                                                            \
-            snprintf(name, sizeof name, "w16s R%d %s ns%d ks%d (%d WGs)", R, TAG, ns, ks, gx * gy * ks);          \
-            printf("  %-40s %8.3f us\n", name, time_graph(w16s_fn<R, ABL>(M, N, K, ns, ks, ws), A, W, C, st));
-            V(2, 0, "full")
-            V(2, 1, "DMA only")
-            V(2, 2, "compute only")
-            V(2, 3, "hand-off only")
+#define V(TT, R, ABL, TAG)                                                                                        \
+            snprintf(name, sizeof name, "w16s TT%d R%d %s ns%d ks%d (%d WGs)", TT, R, TAG, ns, ks,                 \
+                     gx * ((M + 16 * TT - 1) / (16 * TT)) * ks);                                                   \
+            printf("  %-44s %8.3f us\n", name, time_graph(w16s_fn<TT, R, ABL>(M, N, K, ns, ks, ws), A, W, C, st));
+            V(1, 2, 0, "full")
+            V(2, 2, 0, "full")
+            V(2, 3, 0, "full")
+            V(2, 2, 1, "DMA only")
+            V(2, 2, 2, "compute only")
+            V(2, 2, 3, "hand-off only")
 #undef V
             fflush(stdout);
         }
