@@ -222,7 +222,8 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // for at the store, so no kernarg fetch sits in front of the weight stream.
 // ABL (tuning probes only; the product uses 0): bit 1 — no activation staging (records taken from a
 // constant: no A loads, no LDS, no barrier); bit 2 — no dot / epilogue (the weight dwords are summed);
-// bit 4 — nontemporal output stores; bit 8 — write-through (agent-scope, sc1) output stores.
+// bit 4 — nontemporal output stores; bit 8 — write-through (agent-scope, sc1) output stores;
+// bit 16 — M = 1: the workgroup's outputs gathered through LDS into one coalesced store.
 // The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
 // minimal argument list.
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL>
@@ -379,7 +380,17 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
         }
     }
     QG_STAMP(tc);
-    if constexpr (!SUMI) {
+    if constexpr (!SUMI && (ABL & 16) != 0 && MT == 1 && LPR == 64) {
+        // one coalesced store of the workgroup's RPB consecutive outputs (M = 1, unit stride)
+        __shared__ float obuf[WGS / 64];
+        acc[0] = group_sum_last<LPR>(acc[0]);
+        if (lane == 63) obuf[tid >> 6] = acc[0];
+        __syncthreads();
+        if (tid < RPB) {
+            const int r = tile * RPB + tid;
+            if (r < N) C[r] = obuf[tid];
+        }
+    } else if constexpr (!SUMI) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<LPR>(acc[m]);
         if (row_ok && lir == LPR - 1) {
@@ -420,10 +431,13 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
 // entry's 13 preloaded dwords than with these 8 (tools/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
+#ifndef QG_GEMV_WGSTORE
+#define QG_GEMV_WGSTORE 0
+#endif
 template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
-    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, 0>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, QG_GEMV_WGSTORE ? 16 : 0>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 

@@ -642,13 +642,14 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
 // (deterministic) with sc1 loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1).
 // TT: 16-token tiles per workgroup (1: 16 tokens; 2: 32 tokens, each weight fragment decoded once
 // for both token tiles).
-template <int TT> struct w16s_geom {
+template <int TT, int F = FMT_Q4_0> struct w16s_geom {
     static constexpr int ROWS = 128;              // weight rows per workgroup (4 waves x 2 tiles of 16)
     static constexpr int TOK = 16 * TT;           // tokens per workgroup
-    static constexpr int RSB = 4 * 18;            // Q4_0 bytes per row per stage (4 blocks)
-    static constexpr int RIMG = RSB + 8;          // 16-B aligned row window (80 B)
+    static constexpr int BB = wfmt<F>::BB;        // 18 (Q4_0) or 34 (Q8_0): 4 blocks = 8 mod 16 bytes
+    static constexpr int RSB = 4 * BB;            // weight bytes per row per stage (4 blocks)
+    static constexpr int RIMG = RSB + 8;          // 16-B aligned row window (80 / 144 B)
     static constexpr int PPR = RIMG / 16;         // 16-B pieces per row window
-    static constexpr int WP = ROWS * PPR;         // weight pieces per stage (640)
+    static constexpr int WP = ROWS * PPR;         // weight pieces per stage (640 / 1152)
     static constexpr int ATS = 33;                // pieces per token image (32 data + 1 pad)
     static constexpr int AP = TOK * ATS;          // activation pieces per stage
     static constexpr int NI = ((WP + AP + 63) / 64 + 3) / 4 * 4;  // DMA instructions per stage (whole per wave)
@@ -710,6 +711,18 @@ __device__ __forceinline__ u32x4_t w16s_wfrag(uint32_t v) {
                    hi16_pack(__float_as_uint(v2.x), __float_as_uint(v2.y)), hi16_pack(__float_as_uint(v3.x), __float_as_uint(v3.y))};
 }
 
+// Q8_0: k-slot q = signed qs bytes 4q..4q+3 (dword v0) and 16+4q..16+4q+3 (v1) -> 8 exact bf16.
+__device__ __forceinline__ u32x4_t w16s_wfrag_q8(uint32_t v0, uint32_t v1) {
+    const uint32_t a = v0 ^ 0x80808080u, b = v1 ^ 0x80808080u;  // q + 128, unsigned
+    const f32x2 o = {-128.0f, -128.0f};
+    const f32x2 x0 = f32x2{cvt_ubyte<0>(a), cvt_ubyte<1>(a)} + o;
+    const f32x2 x1 = f32x2{cvt_ubyte<2>(a), cvt_ubyte<3>(a)} + o;
+    const f32x2 x2 = f32x2{cvt_ubyte<0>(b), cvt_ubyte<1>(b)} + o;
+    const f32x2 x3 = f32x2{cvt_ubyte<2>(b), cvt_ubyte<3>(b)} + o;
+    return u32x4_t{hi16_pack(__float_as_uint(x0.x), __float_as_uint(x0.y)), hi16_pack(__float_as_uint(x1.x), __float_as_uint(x1.y)),
+                   hi16_pack(__float_as_uint(x2.x), __float_as_uint(x2.y)), hi16_pack(__float_as_uint(x3.x), __float_as_uint(x3.y))};
+}
+
 // ds_write_b128 the compiler does not see: an LDS store it sees makes it wait for every LDS-DMA in
 // flight (vmcnt(0)), which would drain the stage ring (qg_mmq_kernel.hpp). Ordered by "memory"
 // clobbers; completion waited for explicitly (lgkmcnt) before the barrier that publishes it.
@@ -722,9 +735,9 @@ __device__ __forceinline__ void ds_write_x4_asm(uint8_t* p, u32x4_t v) {
 // (for every token tile); lane (r16, q) reads its token's 8 fp32 of k-slot q (elements 4q.. and
 // 16+4q.., two 16-B pieces of the raw image) and writes a = hi + mid + lo (truncated bf16 parts,
 // exact) as three 16-B operand fragments, planes [plane][block][tt][lane] (1 KiB each).
-template <int TT>
+template <int TT, int F>
 __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, int wave, int lane) {
-    using G = w16s_geom<TT>;
+    using G = w16s_geom<TT, F>;
     const int r16 = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
@@ -759,10 +772,10 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
 
 // One 4-block stage of a wave (SH: the data's byte offset in the row windows, 0 on even stages, 8
 // on odd ones). acc[i][t][e]: token 16 t + 4q + e, weight row 32 wave + 16 i + r16.
-template <int TT, int SH>
+template <int TT, int F, int SH>
 __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* planes, int wave, int lane,
                                            f32x4_t (&acc)[2][TT]) {
-    using G = w16s_geom<TT>;
+    using G = w16s_geom<TT, F>;
     const int r16 = lane & 15, q = lane >> 4;
     u32x4_t ap[3][4][TT];
 #pragma unroll
@@ -776,16 +789,22 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
     float dw[4][2];
     static_for<4>([&](auto BI) {
         constexpr int b = decltype(BI)::value;
-        constexpr int X0 = SH + 18 * b + 2;  // qs dword 0 of block b in the row window (+4q for k-slot q)
+        constexpr int X0 = SH + G::BB * b + 2;  // qs[0] of block b in the row window (+4q for k-slot q)
         constexpr int al = X0 % 4;
-        constexpr int D = SH + 18 * b;       // its f16 d
+        constexpr int D = SH + G::BB * b;       // its f16 d
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const uint8_t* row = sb + (32 * wave + 16 * i + r16) * G::RIMG;
             const uint32_t* pw = reinterpret_cast<const uint32_t*>(row + (X0 & ~3) + 4 * q);
             uint32_t v = pw[0];
             if constexpr (al != 0) v = __builtin_amdgcn_alignbyte(pw[1], v, al);
-            wf[b][i] = w16s_wfrag(v);
+            if constexpr (F == FMT_Q8_0) {
+                uint32_t v1 = pw[4];  // qs[16 + 4q ..]
+                if constexpr (al != 0) v1 = __builtin_amdgcn_alignbyte(pw[5], v1, al);
+                wf[b][i] = w16s_wfrag_q8(v, v1);
+            } else {
+                wf[b][i] = w16s_wfrag(v);
+            }
             dw[b][i] = h2f(*reinterpret_cast<const uint16_t*>(row + D));
         }
     });
@@ -832,11 +851,11 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
 // publishes it, and every wave computes the stage. ABL (tuning probes only): 1 = DMA and waits
 // without split / compute, 2 = split + compute on whatever the LDS holds, no DMA, 3 = neither (the
 // launch, barriers and the split-K hand-off alone).
-template <int TT, int R, int ABL>
+template <int TT, int R, int ABL, int F = FMT_Q4_0>
 __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int M, int N, int K, long ldc_m, long ldc_n,
                                                    int ns, float* __restrict__ part, unsigned* __restrict__ cnt) {
-    using G = w16s_geom<TT>;
+    using G = w16s_geom<TT, F>;
     static_assert(R >= 2 && R <= 7, "ring slots (w16s_wait counts up to 7 younger stages)");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -845,7 +864,7 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
     const int nst = K / 128;
     const int h0 = blockIdx.z * ns;
     const int nloc = min(ns, nst - h0);  // stages of this slice
-    const long RB = (long)(K / QK) * 18;
+    const long RB = (long)(K / QK) * G::BB;
     uint8_t* planes = lds + R * G::SBYTES;
 
     // this wave's DMA instructions i = wave + 4 k: piece p = 64 i + lane (clamped into the padding)
@@ -887,12 +906,12 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
         asm volatile("" ::: "memory");
         if (s + AHEAD < nloc) issue(s + AHEAD);  // into the slot of stage s - 1
         if constexpr (ABL != 1 && ABL != 3) {
-            w16s_split<TT>(slot(s), planes, wave, lane);
+            w16s_split<TT, F>(slot(s), planes, wave, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // planes of stage s published
             asm volatile("" ::: "memory");
-            if ((h0 + s) & 1) w16s_stage<TT, 8>(slot(s), planes, wave, lane, acc);
-            else w16s_stage<TT, 0>(slot(s), planes, wave, lane, acc);
+            if ((h0 + s) & 1) w16s_stage<TT, F, 8>(slot(s), planes, wave, lane, acc);
+            else w16s_stage<TT, F, 0>(slot(s), planes, wave, lane, acc);
         }
     }
 
@@ -1093,6 +1112,9 @@ w16_plan w16_make_plan(int M, int N, int K) {
 #ifndef W16S_R
 #define W16S_R 2  // LDS ring slots of w16s_kernel (2: one stage in flight ahead; 3-4 measured slower)
 #endif
+#ifndef QG_W16S_Q8
+#define QG_W16S_Q8 1  // the round-2 prefill for W8A16 (Q8_0 weights) too
+#endif
 #ifndef W16S_TT2
 #define W16S_TT2 0  // 32-token tiles for M > 16 (tuning knob)
 #endif
@@ -1116,24 +1138,24 @@ w16_plan w16s_make_plan(int M, int N, int K) {
     return p;
 }
 
-template <int TT> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
-    using G = w16s_geom<TT>;
+template <int F, int TT> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    using G = w16s_geom<TT, F>;
     unsigned* cnt = (unsigned*)ws;
     float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
     constexpr size_t lds = (size_t)W16S_R * G::SBYTES + G::PLB;
     static_assert(lds <= 160 * 1024, "LDS per workgroup");
     static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)w16s_kernel<TT, W16S_R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = hipFuncSetAttribute((const void*)w16s_kernel<TT, W16S_R, 0, F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
+    hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0, F>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
                        (const uint8_t*)g.B, g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n, p.ns, part, cnt);
     return hipGetLastError();
 }
-hipError_t w16s_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
-    return p.tt == 2 ? w16s_launch_tt<2>(g, p, ws, st) : w16s_launch_tt<1>(g, p, ws, st);
+template <int F> hipError_t w16s_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    return p.tt == 2 ? w16s_launch_tt<F, 2>(g, p, ws, st) : w16s_launch_tt<F, 1>(g, p, ws, st);
 }
 
 template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs& g, const w16_plan& p, void* ws,
@@ -1157,7 +1179,7 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
 }
 
 template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
-    if constexpr (F == FMT_Q4_0) {
+    if constexpr (F == FMT_Q4_0 || (F == FMT_Q8_0 && QG_W16S_Q8)) {
         // round-2 prefill: 16-B aligned activations and weights (rows are then 16-B multiples)
         if (((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && (g.M + 15) / 16 <= 65535) {
             const w16_plan p = w16s_make_plan(g.M, g.N, g.K);
@@ -1167,7 +1189,7 @@ template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
                     if (g.ws) ws = g.ws_bytes >= p.ws_bytes && ((uintptr_t)g.ws & 255) == 0 ? g.ws : nullptr;
                     else ws = stream_workspace(st, p.ws_bytes);
                 }
-                if (ws || p.ks == 1) return w16s_launch(g, p, ws, st);
+                if (ws || p.ks == 1) return w16s_launch<F>(g, p, ws, st);
             }
         }
     }

@@ -32,7 +32,7 @@ CONFIGS = [
     ("q8_0", 1, 4096, 4096), ("q8_0", 32, 4096, 4096),          # W8A8
     ("w4a16", 1, 4096, 4096), ("w4a16", 4, 4096, 4096), ("w4a16", 16, 4096, 4096), ("w4a16", 32, 4096, 4096),
     ("w4a16", 64, 4096, 4096), ("w4a16", 512, 4096, 4096),
-    ("w8a16", 1, 4096, 4096), ("w8a16", 32, 4096, 4096),
+    ("w8a16", 1, 4096, 4096), ("w8a16", 16, 4096, 4096), ("w8a16", 32, 4096, 4096), ("w8a16", 64, 4096, 4096),
 ]
 WT = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7, "q8_0": 8}
 W16 = {"w4a16": 2, "w8a16": 8}
