@@ -176,8 +176,19 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     const int lane = threadIdx.x & 63;
     const int r16 = lane & 15;
     const int q = lane >> 4;
-const int n0 = blockIdx.x * BN;
-    const int m0 = blockIdx.y * G::NTOK;
+#ifndef QG_MMQ_XCDTOK
+#define QG_MMQ_XCDTOK 0
+#endif
+    // (tuning knob) two token tiles on disjoint XCD halves: linear workgroup L runs on XCD L % 8;
+    // XCDs 0-3 take token tile 0, XCDs 4-7 token tile 1, so each XCD's L2 serves one activation tile
+    int tx = blockIdx.x, ty = blockIdx.y;
+    if (QG_MMQ_XCDTOK && gridDim.y == 2 && (gridDim.x & 3) == 0 && gridDim.z == 1) {
+        const int L = blockIdx.y * gridDim.x + blockIdx.x, x8 = L & 7;
+        ty = x8 >> 2;
+        tx = (L >> 3) * 4 + (x8 & 3);
+    }
+    const int n0 = tx * BN;
+    const int m0 = ty * G::NTOK;
     const int nb = K / QK;
     const int H = nb / SB / KS;  // stages of this workgroup's K slice
     const int h0 = KS > 1 ? (int)blockIdx.z * H : 0;
