@@ -53,6 +53,53 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 WTYPES = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
 
 
+def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: int = 10) -> dict:
+    """A BASELINE side config on this GPU the way the headline is measured: step4-recipe data,
+    G launches of the product dispatch (qg_gemm_w4a8, auto) over rotating resident weight copies
+    (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays."""
+    wt = WTYPES[wname]
+    bb = qg.BLOCK_BYTES[wt]
+    a_h, b_h = qhost.fill_step4(M, N, K, 42, 0, N)
+    a, b = torch.from_numpy(a_h).to(dev), torch.from_numpy(b_h).to(dev)
+    del a_h, b_h
+    aq, bq = qg.quantize_q8_1(a), qg.quantize(b, wt)
+    c = qg.gemm_w4a8(aq, bq, M, N, K, wt)
+    ref = a.double() @ b.double().T
+    nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
+    del a, b, ref, c
+    R = max(G, math.ceil(600e6 / bq.numel()))
+    copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
+    copies.copy_(bq.unsqueeze(0).expand_as(copies))
+    out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+
+    def step() -> None:
+        for j in range(G):
+            qg.gemm_w4a8(aq, copies[j], M, N, K, wt, out=out[j])
+
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * G)
+    nbytes = algo_bytes(M, N, K, bb)
+    res = {"wtype": wname, "M": M, "N": N, "K": K, "kernel_algo": int(qg.select_algo(M, N, K, wt)),
+           "us_per_launch": round(us, 3), "gbps": round(nbytes / us / 1e3, 1),
+           "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
+           "nmse_vs_fp32": nmse}
+    del copies, out, g
+    return res
+
+
 def algo_bytes(m: int, n: int, k: int, bb: int) -> int:
     """N*(K/32)*S_w + M*(K/32)*36 + M*N*4 (tests/benchmark/benchmark_comparison.cu:138-140)."""
     nb = k // 32
@@ -155,6 +202,8 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the side measurements of BASELINE configs[2] and [3] (N = 1 only)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -426,6 +475,12 @@ def main() -> None:
                                       for x in mt]
         else:
             out["cpu_baseline"] = None
+        if world == 1 and not args.no_configs and args.wtype == "q4_0" and args.n == 0 and args.m == 1 and args.k == 4096:
+            # BASELINE configs[2] (the M=32 prefill) and configs[3] (all-quants GEMV), measured on the
+            # same GPU in the same run (parity cases otherwise; not part of `value`)
+            torch.cuda.empty_cache()
+            sides = [("q4_0", 32, 4096, 4096), ("q4_1", 1, 4096, 4096), ("q5_0", 1, 4096, 4096), ("q5_1", 1, 4096, 4096)]
+            out["side_configs"] = [measure_config(w, m_, n_, k_, dev) for (w, m_, n_, k_) in sides]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
