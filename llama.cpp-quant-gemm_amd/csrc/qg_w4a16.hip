@@ -642,6 +642,12 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
 // (deterministic) with sc1 loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1).
 // TT: 16-token tiles per workgroup (1: 16 tokens; 2: 32 tokens, each weight fragment decoded once
 // for both token tiles).
+#ifndef QG_W16S_U128
+#define QG_W16S_U128 0  // Q4_0 weight fragments as bf16 128 + q (w16s_wfrag_u128): measured M=16 +0.06,
+                        // M=32 -0.29, M=64 +0.11 us (profiles/r02_tuning/ab_u128.txt) — the stage is not
+                        // VALU-bound once the split is shared; off (exact q - 8 products kept)
+#endif
+
 template <int TT, int F = FMT_Q4_0> struct w16s_geom {
     static constexpr int ROWS = 128;              // weight rows per workgroup (4 waves x 2 tiles of 16)
     static constexpr int TOK = 16 * TT;           // tokens per workgroup
@@ -711,6 +717,16 @@ __device__ __forceinline__ u32x4_t w16s_wfrag(uint32_t v) {
                    hi16_pack(__float_as_uint(v2.x), __float_as_uint(v2.y)), hi16_pack(__float_as_uint(v3.x), __float_as_uint(v3.y))};
 }
 
+// The same k-slot as 8 exact bf16 of 128 + q (QG_W16S_U128): a nibble q under a 0x43 high byte is
+// the bf16 0x430q = 128 + q, so one v_perm_b32 builds two elements (7 VALU per dword instead of 19);
+// the stage subtracts 136 * (the block's activation dot with a constant-136 fragment) — the same
+// MFMA chain on the same activation planes, so a row of zero weights (q = 8) cancels exactly.
+__device__ __forceinline__ u32x4_t w16s_wfrag_u128(uint32_t v) {
+    const uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu, c = 0x43434343u;
+    return u32x4_t{__builtin_amdgcn_perm(c, lo, 0x04010400u), __builtin_amdgcn_perm(c, lo, 0x04030402u),
+                   __builtin_amdgcn_perm(c, hi, 0x04010400u), __builtin_amdgcn_perm(c, hi, 0x04030402u)};
+}
+
 // Q8_0: k-slot q = signed qs bytes 4q..4q+3 (dword v0) and 16+4q..16+4q+3 (v1) -> 8 exact bf16.
 __device__ __forceinline__ u32x4_t w16s_wfrag_q8(uint32_t v0, uint32_t v1) {
     const uint32_t a = v0 ^ 0x80808080u, b = v1 ^ 0x80808080u;  // q + 128, unsigned
@@ -776,6 +792,7 @@ template <int TT, int F, int SH>
 __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* planes, int wave, int lane,
                                            f32x4_t (&acc)[2][TT]) {
     using G = w16s_geom<TT, F>;
+    constexpr bool U128 = QG_W16S_U128 && F == FMT_Q4_0;
     const int r16 = lane & 15, q = lane >> 4;
     u32x4_t ap[3][4][TT];
 #pragma unroll
@@ -802,6 +819,8 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
                 uint32_t v1 = pw[4];  // qs[16 + 4q ..]
                 if constexpr (al != 0) v1 = __builtin_amdgcn_alignbyte(pw[5], v1, al);
                 wf[b][i] = w16s_wfrag_q8(v, v1);
+            } else if constexpr (U128) {
+                wf[b][i] = w16s_wfrag_u128(v);
             } else {
                 wf[b][i] = w16s_wfrag(v);
             }
@@ -810,25 +829,36 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
     });
     __builtin_amdgcn_sched_barrier(0);
     f32x4_t c[4][2][TT];
+    f32x4_t z[4][TT];  // U128: 136 * the block's activation sum, per token (the same for every row)
+    const u32x4_t k136 = {0x43084308u, 0x43084308u, 0x43084308u, 0x43084308u};  // bf16 136
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int t = 0; t < TT; ++t) {
 #pragma unroll
-            for (int t = 0; t < TT; ++t)
+            for (int i = 0; i < 2; ++i)
                 c[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0][b][t]),
                                                                      __builtin_bit_cast(bf16x8_t, wf[b][i]),
                                                                      f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            if constexpr (U128)
+                z[b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0][b][t]),
+                                                                  __builtin_bit_cast(bf16x8_t, k136),
+                                                                  f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
 #pragma unroll
     for (int pl = 1; pl < 3; ++pl)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int t = 0; t < TT; ++t) {
 #pragma unroll
-                for (int t = 0; t < TT; ++t)
+                for (int i = 0; i < 2; ++i)
                     c[b][i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl][b][t]),
                                                                          __builtin_bit_cast(bf16x8_t, wf[b][i]), c[b][i][t], 0, 0, 0);
+                if constexpr (U128)
+                    z[b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl][b][t]),
+                                                                      __builtin_bit_cast(bf16x8_t, k136), z[b][t], 0, 0, 0);
+            }
     // MFMA results read by the VALU behind an explicit wait (8 states needed; qg_mmq_kernel.hpp)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -840,7 +870,10 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
 #pragma unroll
             for (int t = 0; t < TT; ++t)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) acc[i][t][e] = __builtin_fmaf(dw[b][i], c[b][i][t][e], acc[i][t][e]);
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (U128) acc[i][t][e] = __builtin_fmaf(dw[b][i], c[b][i][t][e] - z[b][t][e], acc[i][t][e]);
+                    else acc[i][t][e] = __builtin_fmaf(dw[b][i], c[b][i][t][e], acc[i][t][e]);
+                }
 }
 
 // grid (ceil(N / 128), ceil(M / (16 TT)), ks); slice z = stages [z * ns, min(nst, (z + 1) * ns)) of
