@@ -228,6 +228,38 @@ def block_terms(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_
     return dw * da * fs + mw * sa
 
 
+def block_parts(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_0):
+    """The two exact parts of each block term (float64 [M,N,nb]): the scaled dot d_w*d_a*sumi and
+    the offset part (-8 d_w s_a for Q4_0, -16 d_w s_a for Q5_0, m_w s_a for Q4_1 / Q5_1, 0 for Q8_0);
+    term_b = dot_b + off_b in exact arithmetic (include/gemm_reference.h:202-214)."""
+    da = _h(a_q[..., 0:2]).astype(np.float64)[:, None, :]
+    sa = _h(a_q[..., 2:4]).astype(np.float64)[:, None, :]
+    dw = _h(b_q[..., 0:2]).astype(np.float64)[None, :, :]
+    dot = dw * da * sumi.astype(np.float64)
+    if t == Q4_0:
+        off = -8.0 * dw * sa
+    elif t == Q5_0:
+        off = -16.0 * dw * sa
+    elif t == Q8_0:
+        off = np.zeros_like(dot)
+    else:
+        off = _h(b_q[..., 2:4]).astype(np.float64)[None, :, :] * sa
+    return dot, off
+
+
+def reassoc_tol(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_0, waves: int = 8) -> np.ndarray:
+    """Bound for a kernel that rounds the two parts of each block term separately and sums them
+    on their own (the MFMA prefill's EPI2 epilogue: d_w*d_a*sumi rounded once per block, the offset
+    parts summed by an f16 MFMA and combined at the end, `waves` K-split partial tiles added in fixed
+    order): to first order both the reference and that kernel lie within (nb + waves + 2) u
+    sum_b (|dot_b| + |off_b|) of the exact sum (u = 2^-24), so they differ by at most twice that.
+    Unlike summation_tol this does not assume bit-identical per-block terms: where a block's two
+    parts nearly cancel, its term is small but both parts' rounding errors remain."""
+    dot, off = block_parts(a_q, b_q, sumi, t)
+    nb = dot.shape[-1]
+    return 2.0 * (nb + waves + 2) * 2.0 ** -24 * (np.abs(dot) + np.abs(off)).sum(axis=-1) + 1e-30
+
+
 def summation_tol(a_q: np.ndarray, b_q: np.ndarray, sumi: np.ndarray, t: int = Q4_0) -> np.ndarray:
     """Bound on |fl(sum_b term_b) - fl'(sum_b term_b)| for any two fp32 summation orders
     (2 * nb * 2^-24 * sum_b |term_b|) — the only legitimate CPU/GPU difference once the

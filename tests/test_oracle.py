@@ -266,3 +266,33 @@ def test_recorded_nmse_allquants(O, name, t):
     want = KAT["nmse_vs_fp32"]["allquants_m1_n4096_k4096"][name]
     # printed with 5 significant figures; the FP32 reference's float summation may move the last
     assert abs(O.nmse(c, O.gemm_fp32(a, b)) - want) <= 1.5e-4 * want
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+def test_reassoc_tol_covers_split_epilogue(O, t):
+    """oracle.reassoc_tol (the MFMA prefill's bar) holds for a numpy emulation of that kernel's
+    arithmetic — d_w*d_a formed exactly, times sumi rounded once per block, the offset parts summed
+    on their own, 8 K-split partials added in order, combined at the end — at the small K where
+    summation_tol (which assumes bit-identical per-block terms) is too tight for it."""
+    m, n, k = 24, 40, 128
+    a, b = O.fill_uniform_step4(m, n, k, 3 + t)
+    aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, t)
+    c_ref, s = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    dot, off = O.block_parts(aq, bq, s, t)
+    f32 = np.float32
+    p = dot.astype(f32)                                   # one rounding per block (exact dd * sumi)
+    nb = p.shape[-1]
+    waves = 8
+    acc = np.zeros(p.shape[:2], f32)
+    comp = np.zeros(p.shape[:2], f32)
+    for w in range(waves):                                # K split over waves, partials in order
+        pa = np.zeros(p.shape[:2], f32)
+        pc = np.zeros(p.shape[:2], f32)
+        for bi in range(w, nb, waves):
+            pa = (pa + p[..., bi]).astype(f32)
+            pc = (pc + off[..., bi].astype(f32)).astype(f32)
+        acc = (acc + pa).astype(f32)
+        comp = (comp + pc).astype(f32)
+    got = (acc + comp).astype(f32).astype(np.float64)
+    assert (np.abs(got - c_ref) <= O.reassoc_tol(aq, bq, s, t)).all()
+    assert (O.reassoc_tol(aq, bq, s, t) >= O.summation_tol(aq, bq, s, t)).all()
