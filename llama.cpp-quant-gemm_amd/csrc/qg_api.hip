@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 
 #include "../../include/qg/qg.h"
@@ -21,10 +22,12 @@ using namespace qg;
 namespace qg {
 namespace {
 std::mutex g_ws_mu;
-std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> g_ws;
+// key: (device, stream, slot) — slot 0 the W4A16 split-K workspace (its counters must stay zero
+// between calls), slot 1 the padded-repack buffers of the odd-K/32 prefill (qg_repack.hip)
+std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> g_ws;
 }  // namespace
 
-void* stream_workspace(hipStream_t st, size_t bytes) {
+void* stream_workspace(hipStream_t st, size_t bytes, int slot) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     // Never hand the library's buffer to a stream capture: a graph would keep its raw pointer,
@@ -37,7 +40,7 @@ void* stream_workspace(hipStream_t st, size_t bytes) {
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    auto& e = g_ws[{dev, st}];
+    auto& e = g_ws[std::make_tuple(dev, st, slot)];
     if (e.first && e.second >= bytes) return e.first;
     const size_t sz = std::max(bytes, (size_t)4 << 20);
     void* p = nullptr;
@@ -96,8 +99,10 @@ int select_algo(const GemmArgs& g) {
     if (g.M <= 4 && gemv_eligible(g)) return QG_ALGO_GEMV;
     if (mfma_eligible(g)) return QG_ALGO_MFMA;
     if (gemv_eligible(g)) return QG_ALGO_GEMV;
-    // odd K / 32 (rows off dword alignment) or 2-B aligned weights: one wave per weight row
-    // (qg_ragged.hip) instead of the byte-load generic kernel's one wave per output
+    // odd K / 32 (rows off dword alignment) or 2-B aligned weights at prefill sizes: the MFMA kernel
+    // on a zero-padded copy (qg_repack.hip); below that one wave per weight row (qg_ragged.hip)
+    // instead of the byte-load generic kernel's one wave per output
+    if (repack_eligible(g)) return QG_ALGO_MFMA;
     if (ragged_eligible(g)) return QG_ALGO_RAGGED;
     return QG_ALGO_GENERIC;
 }
@@ -122,6 +127,14 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
             if (g.batch > 65535) return QG_ERR_INVALID_ARG;
             return hip_status(launch_gemv(g, st));
         }
+    }
+    // MFMA on a shape the kernel cannot address directly (odd K / 32, 2-B aligned weights): through
+    // the zero-padded repack; without a workspace (stream capture) the automatic choice falls back
+    if (algo == QG_ALGO_MFMA && !mfma_eligible(g) && repack_eligible(g)) {
+        const hipError_t e = launch_repack_mfma(g, st);
+        if (e != hipErrorNotReady) return hip_status(e);
+        if (!auto_algo) return QG_ERR_UNSUPPORTED;
+        algo = ragged_eligible(g) ? QG_ALGO_RAGGED : QG_ALGO_GENERIC;
     }
     // MFMA and generic kernels take one product per launch: enqueue the batch item by item.
     auto item = [&](int i) {

@@ -49,6 +49,15 @@ hipError_t launch_generic(const GemmArgs& g, hipStream_t st);
 bool ragged_eligible(const GemmArgs& g);
 hipError_t launch_ragged(const GemmArgs& g, hipStream_t st);
 
+// Odd K / 32 at prefill sizes (qg_repack.hip): weights and activations copied into rows padded with
+// zero blocks (d = 0, s = 0) to K'/32 = round_up(K/32, 8), then the MFMA kernel on K'. Every padded
+// term is an exact +0, so each real block's int32 dot and scale product is what the MFMA kernel
+// computes at any aligned K; the sumi hook runs the same MFMA instantiation into a padded image and
+// compacts it. repack_eligible: shape rules only (pointers not needed).
+bool repack_eligible(const GemmArgs& g);
+// returns hipErrorNotReady (nothing enqueued) when no workspace can be had right now (e.g. capture)
+hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st);
+
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.
 // g.ws / g.ws_bytes: optional caller workspace for the split-K prefill (>= w16_workspace_bytes,
 // 256-B aligned, zero before its first use; left zero by every launch).
@@ -63,7 +72,7 @@ hipError_t launch_fp32(const GemmArgs& g, hipStream_t st);
 // one stream are ordered, and every split-K launch leaves its counters zero). nullptr when it
 // cannot be allocated right now (e.g. the stream is being captured): callers fall back to a
 // kernel without a workspace.
-void* stream_workspace(hipStream_t st, size_t bytes);
+void* stream_workspace(hipStream_t st, size_t bytes, int slot = 0);
 
 // Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);

@@ -1,0 +1,128 @@
+// qg_repack.hip — odd K / 32 at prefill sizes through the MFMA kernel.
+//
+// With K/32 odd, every other weight row starts 2 bytes off a dword, which the MFMA kernel's LDS-DMA
+// pieces cannot address; the ragged kernel (qg_ragged.hip) serves those shapes with one wave per
+// weight row and no matrix cores (K = 4128: 24.6 us at M = 32, 45.9 us at M = 64 against 6-9 us for
+// the MFMA kernel on the same bytes; tools/repack_probe.py, profiles/r02_tuning/repack_probe.txt).
+// Here one streaming kernel copies the weights [N][K/32] and the activations [M][K/32] into rows of
+// K'/32 = round_up(K/32, 8) blocks in a per-stream workspace, the extra blocks all zero bytes
+// (d = 0 and s = 0: each padded term of gemm_reference.h:202-212 is an exact +0), and the MFMA
+// kernel runs on K' (8-block rows also give it the 16-B piece form, P16). The sumi parity hook
+// runs the same MFMA instantiation into a [M][N][K'/32] image and compacts it to [M][N][K/32].
+#include "qg_common.hpp"
+#include "qg_kernels.hpp"
+
+namespace qg {
+
+namespace {
+constexpr int PADB = 8;  // pad K/32 up to a multiple of this many blocks
+
+int wbytes(int t) {
+    switch (t) {
+        case FMT_Q4_0: return 18;
+        case FMT_Q4_1: return 20;
+        case FMT_Q5_0: return 22;
+        case FMT_Q5_1: return 24;
+        case FMT_Q8_0: return 34;
+    }
+    return 0;
+}
+
+// One thread per 8-byte word of the padded images (weights first, then activations). Sources are
+// 2-B aligned (every block size is even, and so is every row's byte length): four u16 loads per
+// word, zero past the row's real bytes.
+__global__ __launch_bounds__(256) void repack_pad_kernel(const uint16_t* __restrict__ B, uint64_t* __restrict__ Bp,
+                                                         long wwords, int rb, int rbp,
+                                                         const uint16_t* __restrict__ A, uint64_t* __restrict__ Ap,
+                                                         long awords, int ab, int abp) {
+    long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const uint16_t* src = B;
+    uint64_t* dst = Bp;
+    int sb = rb, db = rbp;
+    if (i >= wwords) {
+        i -= wwords;
+        if (i >= awords) return;
+        src = A; dst = Ap; sb = ab; db = abp;
+    }
+    const int wpr = db / 8;
+    const long row = i / wpr;
+    const int off = (int)(i - row * wpr) * 8;  // byte offset in the padded row
+    const uint16_t* s = src + (row * sb + off) / 2;
+    uint64_t v = 0;
+    if (off + 8 <= sb) {
+        v = (uint64_t)s[0] | ((uint64_t)s[1] << 16) | ((uint64_t)s[2] << 32) | ((uint64_t)s[3] << 48);
+    } else {
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+            if (off + 2 * h < sb) v |= (uint64_t)s[h] << (16 * h);
+    }
+    dst[i] = v;
+}
+
+// sumi image [M][N][nbp] -> [M][N][nb]
+__global__ __launch_bounds__(256) void sumi_compact_kernel(const int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                                                           long total, int nb, int nbp) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const long r = i / nb;
+    dst[i] = src[r * nbp + (i - r * nb)];
+}
+
+inline long round256(long x) { return (x + 255) / 256 * 256; }
+
+GemmArgs padded(const GemmArgs& g) {
+    GemmArgs g2 = g;
+    const int nbp = (g.K / QK + PADB - 1) / PADB * PADB;
+    g2.K = nbp * QK;
+    return g2;
+}
+}  // namespace
+
+// Prefill shapes only (the ragged kernel is faster below M = 16: 8.0 vs ~11 us at M = 8) and
+// enough weight rows to amortise the copy; one product per call; the padded MFMA shape must be
+// one the MFMA kernel takes (checked with placeholder 256-B aligned pointers).
+bool repack_eligible(const GemmArgs& g) {
+    if (g.batch != 1 || g.M < 16 || g.N < 1024 || g.ain != AIN_Q8_1 || g.K % QK != 0) return false;
+    if (wbytes(g.wtype) == 0 || ((uintptr_t)g.A & 1) != 0 || ((uintptr_t)g.B & 1) != 0) return false;
+    const long nbp = (g.K / QK + PADB - 1) / PADB * PADB;
+    if ((long)g.N * nbp * wbytes(g.wtype) >= (1L << 40)) return false;
+    GemmArgs g2 = padded(g);
+    g2.A = reinterpret_cast<const void*>(256);
+    g2.B = reinterpret_cast<const void*>(256);
+    return mfma_eligible(g2);
+}
+
+hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st) {
+    GemmArgs g2 = padded(g);
+    const int nb = g.K / QK, nbp = g2.K / QK;
+    const int rb = nb * wbytes(g.wtype), rbp = nbp * wbytes(g.wtype);
+    const int ab = nb * Q8_1_BYTES, abp = nbp * Q8_1_BYTES;
+    const long wimg = round256((long)g.N * rbp), aimg = round256((long)g.M * abp);
+    const long simg = g.sumi ? round256((long)g.M * g.N * nbp * 4) : 0;
+    if (g.describe) {  // configuration query: the MFMA instantiation this call would run
+        g2.A = reinterpret_cast<const void*>(256);
+        g2.B = reinterpret_cast<const void*>(256);
+        return launch_mfma(g2, st);
+    }
+    uint8_t* ws = static_cast<uint8_t*>(stream_workspace(st, (size_t)(wimg + aimg + simg), 1));
+    if (!ws) return hipErrorNotReady;
+    const long wwords = (long)g.N * rbp / 8, awords = (long)g.M * abp / 8;
+    const long blocks = (wwords + awords + 255) / 256;
+    if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(repack_pad_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                       static_cast<const uint16_t*>(g.B), reinterpret_cast<uint64_t*>(ws), wwords, rb, rbp,
+                       static_cast<const uint16_t*>(g.A), reinterpret_cast<uint64_t*>(ws + wimg), awords, ab, abp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    g2.B = ws;
+    g2.A = ws + wimg;
+    if (g.sumi) g2.sumi = reinterpret_cast<int32_t*>(ws + wimg + aimg);
+    e = launch_mfma(g2, st);
+    if (e != hipSuccess || !g.sumi) return e;
+    const long total = (long)g.M * g.N * nb;
+    hipLaunchKernelGGL(sumi_compact_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       g2.sumi, g.sumi, total, nb, nbp);
+    return hipGetLastError();
+}
+
+}  // namespace qg

@@ -276,6 +276,45 @@ def test_ragged_odd_blocks(O, qg, t, m, n, k):
     assert (np.abs(cg.astype(np.float64) - c_ref) <= tol).all()
 
 
+REPACK = [(32, 1100, 4128), (16, 1024, 1056), (20, 1536, 96), (64, 1030, 4128)]
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+@pytest.mark.parametrize("m,n,k", REPACK)
+def test_repack_mfma_odd_blocks(O, qg, t, m, n, k):
+    """Odd K/32 at prefill sizes (M >= 16, N >= 1024): the MFMA kernel on a zero-padded copy
+    (qg_repack.hip). The sumi hook runs that instantiation (padded image compacted to [M][N][K/32])
+    and is bit-exact; outputs sit within the summation bound and agree with the ragged kernel's."""
+    assert qg.select_algo(m, n, k, t) == 2
+    prod = qg.debug_config(m, n, k, t)
+    assert prod.startswith("mmq ") and prod == qg.debug_config(m, n, k, t, sumi=True)
+    aq, bq = random_blocks(np.random.default_rng(m * 7 + n + k + t), m, n, k, t)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t))
+    c_ref, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t))
+    tol = O.reassoc_tol(aq, bq, want, t)
+    assert (np.abs(c.astype(np.float64) - c_ref) <= tol).all()
+    c_rag = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t, algo=4))
+    assert (np.abs(c_rag.astype(np.float64) - c_ref) <= O.summation_tol(aq, bq, want, t)).all()
+    # twice more on the same stream (workspace reused): bit-identical
+    assert np.array_equal(host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t)), c)
+
+
+def test_repack_two_byte_aligned_weights(O, qg):
+    """2-B aligned weight tensor at a prefill size: the repack takes it too (Q4_0, even K/32)."""
+    import torch
+    m, n, k, t = 16, 1024, 4096, 2
+    aq, bq = random_blocks(np.random.default_rng(5), m, n, k, t)
+    raw = torch.zeros(bq.size + 2, dtype=torch.uint8, device="cuda")
+    raw[2:] = dev(bq.ravel())
+    bmis = raw[2:].view(bq.shape)
+    c_mis = host(qg.gemm_w4a8(dev(aq), bmis, m, n, k, t))
+    c_al = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t))
+    close_to_oracle(O, c_mis, aq, bq, t)
+    close_to_oracle(O, c_al, aq, bq, t)
+
+
 @pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
 def test_ragged_two_byte_aligned_weights(O, qg, t):
     """A weight tensor starting 2 bytes past a dword (even K/32 too): GEMV / MFMA decline it, the

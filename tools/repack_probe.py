@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Probe (tuning only; not product): odd K/32 at prefill sizes — the ragged kernel vs a padded
+"""Probe (tuning only; not product): odd K/32 at prefill sizes — the auto dispatch (ragged kernel, or since
+qg_repack.hip the product repack + MFMA at M >= 16, N >= 1024; its kernel family is printed) vs a padded
 repack (weights and activations copied into rows of K'/32 = round_up(K/32, --pad) blocks, the extra
 blocks all zero: d = 0, s = 0) followed by the MFMA kernel on K'. DESIGN.md §9 "Odd K/32".
 
@@ -12,6 +13,7 @@ oracle-free fp32 bound of the ragged result (max |diff| printed).
   python tools/repack_probe.py [--k 4128] [--ms 8,16,32,64] [--wtype 2]
 """
 import argparse
+import ctypes
 import math
 import os
 import sys
@@ -41,6 +43,22 @@ def timed(fn, launches: int) -> float:
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     g.replay()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / launches
+
+
+def timed_eager(fn, launches: int) -> float:
+    """Per-call time of eager back-to-back calls (no capture: the library's repack workspace is
+    never handed to a stream capture, so captured calls fall back to the ragged kernel)."""
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for i in range(launches):
+        fn(i)
     e1.record(st)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1e3 / launches
@@ -89,6 +107,15 @@ def main() -> None:
             repack(i)
             mfma_only(i)
 
+        lib = qg._lib.load()
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        xa, oa = ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr())
+        wa = [ctypes.c_void_p(wc[i].data_ptr()) for i in range(R)]
+
+        def auto_eager(i):  # the C-ABI directly (host cost per call well under the GPU time)
+            lib.qg_gemm_w4a8_ldc(xa, wa[i % R], oa, M, N, K, N, t, 0, sp)
+
+        t_e = timed_eager(auto_eager, a.launches)
         cfg_r = qg.debug_config(M, N, K, t)
         cfg_p = qg.debug_config(M, N, Kp, t, algo=qg.ALGO_MFMA)
         t_r = timed(ragged, a.launches)
@@ -100,7 +127,7 @@ def main() -> None:
         torch.cuda.synchronize()
         d = (out - out2).abs().max().item()
         scale = out.abs().max().item()
-        print(f"M={M:3d}  ragged {t_r:7.2f} us [{cfg_r.split(' ')[0]}]  repack(torch copy) {t_c:6.2f} us"
+        print(f"M={M:3d}  auto eager {t_e:7.2f} us  graph {t_r:7.2f} us [{cfg_r.split(' ')[0]}]  repack(torch copy) {t_c:6.2f} us"
               f"  mfma(K') {t_m:6.2f} us [{cfg_p.split(' ')[0]}]  repack+mfma {t_b:7.2f} us"
               f"  max|diff| {d:.3g} (max|C| {scale:.3g})")
 
