@@ -78,11 +78,12 @@ GemmArgs padded(const GemmArgs& g) {
 }
 }  // namespace
 
-// Prefill shapes only (the ragged kernel is faster below M = 16: 8.0 vs ~11 us at M = 8) and
+// Prefill shapes only (M >= 32: at M = 16 the ragged kernel is as fast, 13.9 vs 13.7 us for Q4_0,
+// and faster for Q8_0, 15.2 vs 16.5 us; profiles/r02_tuning/repack_probe.txt) and
 // enough weight rows to amortise the copy; one product per call; the padded MFMA shape must be
 // one the MFMA kernel takes (checked with placeholder 256-B aligned pointers).
 bool repack_eligible(const GemmArgs& g) {
-    if (g.batch != 1 || g.M < 16 || g.N < 1024 || g.ain != AIN_Q8_1 || g.K % QK != 0) return false;
+    if (g.batch != 1 || g.M < 32 || g.N < 1024 || g.ain != AIN_Q8_1 || g.K % QK != 0) return false;
     if (wbytes(g.wtype) == 0 || ((uintptr_t)g.A & 1) != 0 || ((uintptr_t)g.B & 1) != 0) return false;
     const long nbp = (g.K / QK + PADB - 1) / PADB * PADB;
     if ((long)g.N * nbp * wbytes(g.wtype) >= (1L << 40)) return false;

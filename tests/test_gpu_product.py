@@ -276,13 +276,13 @@ def test_ragged_odd_blocks(O, qg, t, m, n, k):
     assert (np.abs(cg.astype(np.float64) - c_ref) <= tol).all()
 
 
-REPACK = [(32, 1100, 4128), (16, 1024, 1056), (20, 1536, 96), (64, 1030, 4128)]
+REPACK = [(32, 1100, 4128), (32, 1024, 1056), (40, 1536, 96), (64, 1030, 4128)]
 
 
 @pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
 @pytest.mark.parametrize("m,n,k", REPACK)
 def test_repack_mfma_odd_blocks(O, qg, t, m, n, k):
-    """Odd K/32 at prefill sizes (M >= 16, N >= 1024): the MFMA kernel on a zero-padded copy
+    """Odd K/32 at prefill sizes (M >= 32, N >= 1024): the MFMA kernel on a zero-padded copy
     (qg_repack.hip). The sumi hook runs that instantiation (padded image compacted to [M][N][K/32])
     and is bit-exact; outputs sit within the summation bound and agree with the ragged kernel's."""
     assert qg.select_algo(m, n, k, t) == 2
@@ -304,7 +304,7 @@ def test_repack_mfma_odd_blocks(O, qg, t, m, n, k):
 def test_repack_two_byte_aligned_weights(O, qg):
     """2-B aligned weight tensor at a prefill size: the repack takes it too (Q4_0, even K/32)."""
     import torch
-    m, n, k, t = 16, 1024, 4096, 2
+    m, n, k, t = 32, 1024, 4096, 2
     aq, bq = random_blocks(np.random.default_rng(5), m, n, k, t)
     raw = torch.zeros(bq.size + 2, dtype=torch.uint8, device="cuda")
     raw[2:] = dev(bq.ravel())
