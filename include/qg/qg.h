@@ -51,7 +51,8 @@ typedef enum {
 /* Kernel family selection for qg_gemm_w4a8_ex (QG_ALGO_AUTO picks by shape). */
 typedef enum {
     QG_ALGO_AUTO = 0,
-    QG_ALGO_GEMV = 1,    /* M <= 8 (auto: M <= 4): register-resident block decode + v_dot4 */
+    QG_ALGO_GEMV = 1,    /* M <= 8 (auto: M <= 4): register-resident weight units; Q4_0/Q4_1 nibble-plane
+                            v_dot8_u32_u4 / v_dot8_i32_i4, Q5_x/Q8_0 byte decode + v_dot4 */
     QG_ALGO_MFMA = 2,    /* any M (auto: M >= 5), K % 128 == 0: v_mfma_i32_16x16x32_i8 per Q-block */
     QG_ALGO_GENERIC = 3, /* any K % 32 == 0, any alignment: byte loads, one wave per output (cross-check) */
     QG_ALGO_RAGGED = 4   /* any K % 32 == 0 (odd K / 32), 2-B aligned weights: one wave per weight row */
@@ -70,6 +71,15 @@ int qg_gemm_w4a8_ex(const void* A_q8_1, const void* B, float* C, int M, int N, i
  * column slice of a wider buffer in the row-sharded multi-GPU path, quant_gemm/sharded.py). */
 int qg_gemm_w4a8_ldc(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int64_t ldc, int wtype,
                      int algo, qg_stream_t stream);
+
+/* The Solution entry point of the definition gemm_q4_0_q8_1_w4a8
+ * (schemas/definitions/gemm/gemm_q4_0_q8_1_w4a8.json:35-53: inputs A_q8_1[M][K/32], B_q4_0[N][K/32],
+ * output C[M][N]; destination-passing, schemas/docs/solution.md:27-42), in definition order —
+ * the role include/gemm_cuda_dp4a.cuh::gemm_q4_0_q8_1_dp4a plays for the reference's CUDA
+ * solutions (schemas/solutions/gemm_q4_0_q8_1_cuda_dp4a.json:15). == qg_gemm_w4a8(..., QG_TYPE_Q4_0).
+ * Registered by integration/solutions/gemm_q4_0_q8_1_hip_gfx950.json. */
+int qg_gemm_q4_0_q8_1_w4a8(const void* A_q8_1, const void* B_q4_0, float* C, int M, int N, int K,
+                           qg_stream_t stream);
 
 /* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
  * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of

@@ -371,6 +371,11 @@ int qg_gemm_w4a8(const void* A, const void* B, float* C, int M, int N, int K, in
     return qg_gemm_w4a8_ex(A, B, C, M, N, K, wtype, QG_ALGO_AUTO, stream);
 }
 
+int qg_gemm_q4_0_q8_1_w4a8(const void* A_q8_1, const void* B_q4_0, float* C, int M, int N, int K,
+                           qg_stream_t stream) {
+    return qg_gemm_w4a8_ex(A_q8_1, B_q4_0, C, M, N, K, QG_TYPE_Q4_0, QG_ALGO_AUTO, stream);
+}
+
 int qg_gemm_q4_0_q8_1(const void* W, const void* A, float* out, int M, int N, int K, qg_stream_t s) {
     return weight_major(QG_TYPE_Q4_0, W, A, out, M, N, K, s);
 }

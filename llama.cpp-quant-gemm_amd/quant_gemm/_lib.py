@@ -25,6 +25,7 @@ P, I, I64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
 SIGNATURES = {
     "qg_gemm_w4a8": ([P, P, P, I, I, I, I, P], I),
     "qg_gemm_w4a8_ex": ([P, P, P, I, I, I, I, I, P], I),
+    "qg_gemm_q4_0_q8_1_w4a8": ([P, P, P, I, I, I, P], I),
     "qg_gemm_w4a8_ldc": ([P, P, P, I, I, I, I64, I, I, P], I),
     "qg_debug_config": ([I, I, I, I, I, I, ctypes.c_char_p, SZ], I),
     "qg_gemm_w4a8_strided_batched": ([P, I64, P, I64, P, I64, I, I, I, I, I, P], I),
