@@ -18,10 +18,23 @@ Workload:
   * roofline.achieved = algorithmic bytes of ONE launch / its average duration, measured live with
     HIP events on the launch stream over the timed graph replays (so it includes each launch's
     dispatch boundary; rocprofv3's kernel-only durations are committed under profiles/).
-  * "batched": the same G GEMVs issued as ONE qg_gemm_w4a8_strided_batched launch per step.
+  * "batched": the same G GEMVs issued as ONE qg_gemm_w4a8_strided_batched launch per step;
+    "grouped": the same through the pointer-array entry qg_gemm_w4a8_grouped (independent B / C
+    pointers per item, what a decoder layer's Q / K / V or gate / up projections can use).
+  * roofline.floor_us / floor_frac: the single-launch floor under the same protocol (libqg_calib.so:
+    an empty kernel with the GEMV's grid, and the best pure coalesced read of the same algorithmic
+    bytes per launch over the same rotating copies) — what ONE isolated launch of this size can reach.
+  * N=1 side configs: BASELINE configs[2] and [3], and configs[4]'s full N=32000 GEMV on ONE GPU as
+    single launches and as one grouped launch of G — the denominators of the strong-scaling ratios.
+  * N>1 "strong": the N=32000 GEMV split over the ranks (32000/N rows each), timed per step with
+    the all-gather, as G single launches and as one grouped launch per step; the 1-GPU N=32000
+    times measured in the same run on each rank's own GPU; strong_speedup_vs_1gpu_n32000 =
+    1-GPU time per GEMV / N-GPU time per GEMV, per leg.
   * cpu_baseline (rank 0, N=1): the oracle's restatement of gemm_w4a8_reference
-    (include/gemm_reference.h:175-222) on the step4 input recipe, 1 thread, ~10 s sample; plus
-    row-partitioned runs at 16 threads and at nproc (cpu_baseline_mt).
+    (include/gemm_reference.h:175-222) on the step4 input recipe, 1 thread pinned, ~10 s sample;
+    beside it the product's own host twin (libqg_host.so qg_gemm_w4a8_cpu_mt) at 1 pinned thread
+    (cpu_baseline_twin) and row-partitioned over its persistent worker pool at 16 threads and at
+    nproc (cpu_baseline_mt), each with median / p10 / p90.
   * data: the reference's step4 recipe (glibc srand(42), A then B, U[-1,1]) — the NMSE printed is
     then comparable to the reference's own 4.56e-3 at configs[1].
   * the kernel launches go through quant_gemm.sharded.RowShardedW4A8.compute_local (the shipped
@@ -53,10 +66,33 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 WTYPES = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7}
 
 
-def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: int = 10) -> dict:
+def graph_time_us(fn, reps: int = 10, per: int = 1) -> float:
+    """fn() enqueues launches on the current stream; captured once as a hipGraph, replayed `reps`
+    times between HIP events on the launch stream; returns us per launch (per = launches in fn)."""
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    del g
+    return e0.elapsed_time(e1) * 1e3 / (reps * per)
+
+
+def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: int = 10,
+                   forms: tuple = ("single",)) -> list:
     """A BASELINE side config on this GPU the way the headline is measured: step4-recipe data,
     G launches of the product dispatch (qg_gemm_w4a8, auto) over rotating resident weight copies
-    (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays."""
+    (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays.
+    forms: "single" (G launches), "batched" (one qg_gemm_w4a8_grouped launch over the G copies)."""
     wt = WTYPES[wname]
     bb = qg.BLOCK_BYTES[wt]
     a_h, b_h = qhost.fill_step4(M, N, K, 42, 0, N)
@@ -71,33 +107,64 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
     copies.copy_(bq.unsqueeze(0).expand_as(copies))
     out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
-
-    def step() -> None:
-        for j in range(G):
-            qg.gemm_w4a8(aq, copies[j], M, N, K, wt, out=out[j])
-
-    side = torch.cuda.Stream()
-    with torch.cuda.stream(side):
-        step()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        step()
-    g.replay()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / (reps * G)
     nbytes = algo_bytes(M, N, K, bb)
-    res = {"wtype": wname, "M": M, "N": N, "K": K, "kernel_algo": int(qg.select_algo(M, N, K, wt)),
-           "us_per_launch": round(us, 3), "gbps": round(nbytes / us / 1e3, 1),
-           "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
-           "nmse_vs_fp32": nmse}
-    del copies, out, g
+    res = []
+    for form in forms:
+        if form == "single":
+            def step() -> None:
+                for j in range(G):
+                    qg.gemm_w4a8(aq, copies[j], M, N, K, wt, out=out[j])
+        else:
+            def step() -> None:
+                qg.gemm_w4a8_grouped([aq] * G, [copies[j] for j in range(G)], [N] * G, M, K, wt,
+                                     outs=[out[j] for j in range(G)])
+        us = graph_time_us(step, reps, G)
+        res.append({"wtype": wname, "M": M, "N": N, "K": K, "form": form,
+                    "kernel_algo": int(qg.select_algo(M, N, K, wt)),
+                    "us_per_launch" if form == "single" else "us_per_gemv": round(us, 3),
+                    "gbps": round(nbytes / us / 1e3, 1),
+                    "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
+                    "nmse_vs_fp32": nmse})
+    del copies, out
     return res
+
+
+def measure_floor(dev, wcopies: torch.Tensor, G: int, launch_bytes: int, grid: int, block: int) -> dict:
+    """The single-launch floor under the headline's protocol (hipGraph of G back-to-back launches,
+    HIP events on the launch stream): an empty kernel with the GEMV's grid and block, and the
+    fastest pure coalesced read of the GEMV's algorithmic bytes per launch over the same rotating
+    weight copies (libqg_calib.so, include/qg/qg_calib.h)."""
+    lib = ctypes.CDLL(os.path.join(REPO, "llama.cpp-quant-gemm_amd", "quant_gemm", "libqg_calib.so"))
+    lib.qg_calib_empty.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.qg_calib_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    R = wcopies.shape[0]
+    stride = wcopies[0].numel()
+    nbytes = (launch_bytes + 15) // 16 * 16
+    # copies are contiguous: a read of launch_bytes from copy j stays inside the allocation for j < R-1
+    bases = [wcopies.data_ptr() + (j % (R - 1)) * stride for j in range(G)]
+
+    def empty() -> None:
+        cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for _ in range(G):
+            if lib.qg_calib_empty(grid, block, cs) != 0:
+                raise RuntimeError("qg_calib_empty failed")
+
+    def reader(p: int, blk: int):
+        def fn() -> None:
+            cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for j in range(G):
+                if lib.qg_calib_read(ctypes.c_void_p(bases[j]), nbytes, p, blk, ctypes.c_void_p(sink.data_ptr()), cs) != 0:
+                    raise RuntimeError("qg_calib_read failed")
+        return fn
+
+    empty_us = min(graph_time_us(empty, 10, G) for _ in range(3))
+    reads = {f"x4 p{p} wg{blk}": min(graph_time_us(reader(p, blk), 10, G) for _ in range(3))
+             for (p, blk) in ((1, 512), (1, 1024), (2, 512), (2, 1024), (4, 256))}
+    best = min(reads, key=reads.get)
+    return {"empty_us": round(empty_us, 3), "read_us": round(reads[best], 3), "read_config": best,
+            "read_all_us": {k: round(v, 3) for k, v in reads.items()}, "grid": grid, "block": block}
 
 
 def algo_bytes(m: int, n: int, k: int, bb: int) -> int:
@@ -133,12 +200,28 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def _timed_runs(fn, seconds: float):
+    fn()  # warm-up
+    times, t0 = [], time.perf_counter()
+    while True:
+        r0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - r0)
+        if time.perf_counter() - t0 >= seconds:
+            break
+    times.sort()
+    n = len(times)
+    return times[n // 2], times[n // 10], times[(9 * n) // 10], n, time.perf_counter() - t0
+
+
 def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
     """the reference is single-threaded -> the headline baseline is 1 core, pinned
-    (sched_setaffinity, as taskset), after 1 warm-up, median of the runs; plus a row-partitioned
-    multi-thread run. Bounded to ~`seconds` of CPU work."""
+    (sched_setaffinity, as taskset), after 1 warm-up, median of the runs; beside it the product's
+    host twin (libqg_host.so) at 1 pinned thread and row-partitioned over its persistent worker pool.
+    Bounded to ~`seconds` (+ 2 x seconds/5) of CPU work."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O  # the checker / CPU baseline only
+    import numpy as np
     a, b = O.fill_uniform_step4(m, n, k, 42)
     aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, wtype)
     saved = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
@@ -146,45 +229,138 @@ def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
     if core is not None:
         os.sched_setaffinity(0, {core})
     try:
-        O.gemm_w4a8(aq, bq, wtype)  # warm-up
-        times, t0 = [], time.perf_counter()
-        while True:
-            r0 = time.perf_counter()
-            O.gemm_w4a8(aq, bq, wtype)
-            times.append(time.perf_counter() - r0)
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
+        per, p10, p90, runs, el = _timed_runs(lambda: O.gemm_w4a8(aq, bq, wtype), seconds)
+        twin = _timed_runs(lambda: qhost.gemm_w4a8(aq, bq, m, n, k, wtype, 1), seconds / 5)
     finally:
         if saved is not None:
             os.sched_setaffinity(0, saved)
-    times.sort()
-    runs = len(times)
-    per = times[runs // 2]
+    if not np.array_equal(qhost.gemm_w4a8(aq, bq, m, n, k, wtype, 1), O.gemm_w4a8(aq, bq, wtype)):
+        raise RuntimeError("host twin differs from the oracle")
     flops = 2.0 * m * n * k
     model = cpu_model()
-    # row-partitioned runs: at 16 threads (the box's CPU share for one GPU) and at nproc (every
-    # core this process may use)
+    ms3 = lambda t: [round(x * 1e3, 4) for x in t]
+    twin_row = {"value": flops / twin[0] / 1e12, "unit": "TFLOPS", "cores": 1, "kind": "port",
+                "ms_per_gemv": twin[0] * 1e3, "ms_p10_p90": ms3(twin[1:3]), "cpu": model,
+                "sample": f"the product's host twin libqg_host.so qg_gemm_w4a8_cpu_mt (restates "
+                          f"include/gemm_reference.h:175-222), 1 thread pinned to core {core}, median of {twin[3]} runs"}
+    # row-partitioned runs over the twin's persistent pool: 16 threads (the box's CPU share for one
+    # GPU) and nproc (every core this process may use)
     nproc = len(saved) if saved else (os.cpu_count() or 1)
     mts = []
     for threads in sorted({min(16, nproc), nproc}):
-        t1 = time.perf_counter()
-        mt_times = []
-        while time.perf_counter() - t1 < max(1.0, seconds / 5):
-            r0 = time.perf_counter()
-            O.gemm_w4a8_mt(aq, bq, wtype, threads)
-            mt_times.append(time.perf_counter() - r0)
-        mt_times.sort()
-        per_mt = mt_times[len(mt_times) // 2]
-        mts.append({"value": flops / per_mt / 1e12, "unit": "TFLOPS", "cores": threads, "ms_per_gemv": per_mt * 1e3,
-                    "cpu": model, "sample": f"row-partitioned over {threads} threads (nproc {nproc}), "
-                                            f"median of {len(mt_times)} runs"})
+        mt = _timed_runs(lambda: qhost.gemm_w4a8(aq, bq, m, n, k, wtype, threads), max(1.0, seconds / 5))
+        mts.append({"value": flops / mt[0] / 1e12, "unit": "TFLOPS", "cores": threads, "ms_per_gemv": mt[0] * 1e3,
+                    "ms_p10_p90": ms3(mt[1:3]), "cpu": model,
+                    "sample": f"libqg_host.so row-partitioned over a persistent pool of {threads} threads "
+                              f"(nproc {nproc}), median of {mt[3]} runs"})
     return ({"value": flops / per / 1e12, "unit": "TFLOPS", "cores": 1, "kind": "port",
-             "ms_per_gemv": per * 1e3, "ms_p10_p90": [times[runs // 10] * 1e3, times[(9 * runs) // 10] * 1e3],
-             "cpu": model,
+             "ms_per_gemv": per * 1e3, "ms_p10_p90": ms3((p10, p90)), "cpu": model,
              "sample": f"oracle/qg_oracle.c gemm_w4a8 (restates include/gemm_reference.h:175-222), "
                        f"M={m} N={n} K={k}, median of {runs} runs in {el:.1f} s, 1 thread pinned to core "
-                       f"{core}, step4 srand(42) inputs"}, mts)
+                       f"{core}, step4 srand(42) inputs"}, twin_row, mts)
+
+
+def sharded_leg(mods, aq, M: int, G: int, rows: int, world: int, steps: int, warmup: int, form: str, dev) -> dict:
+    """Time one multi-GPU leg: per step G independent GEMVs on this rank's row shard (form
+    "per_launch": G launches through RowShardedW4A8.compute_local; "batched": one grouped launch
+    through RowShardedW4A8.compute_local_group), captured as a hipGraph, then the step's output
+    slices all-gathered asynchronously (overlapping the next step's kernels), double-buffered.
+    Returns the wall time per GEMV (max over ranks) and the event-timed launch-stream time."""
+    R = len(mods)
+    outs = [torch.zeros((G, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world, G, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+
+    def step(s: int) -> None:
+        if form == "per_launch":
+            for j in range(G):
+                mods[j % R].compute_local(aq, M, outs[s][j])
+        else:
+            RowShardedW4A8.compute_local_group([mods[j % R] for j in range(G)], aq, M, outs[s])
+
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        step(0)
+        step(1)
+    torch.cuda.synchronize()
+    graphs = []
+    for s in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step(s)
+        graphs.append(g)
+    pending = [None, None]
+
+    def run(i: int) -> None:
+        s = i % 2
+        if pending[s] is not None:
+            pending[s].wait()
+            pending[s] = None
+        graphs[s].replay()
+        if world > 1:
+            pending[s] = mods[0].gather(outs[s], gathered[s], async_op=True)
+
+    def drain() -> None:
+        for s in range(2):
+            if pending[s] is not None:
+                pending[s].wait()
+                pending[s] = None
+
+    for i in range(warmup):
+        run(i)
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for i in range(steps):
+        run(i)
+    ev1.record()
+    drain()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    launch_us = ev0.elapsed_time(ev1) * 1e3 / (steps * G)
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    del graphs
+    return {"us_per_gemv": round(elapsed / (steps * G) * 1e6, 3), "launch_stream_us_per_gemv": round(launch_us, 3)}
+
+
+def strong_legs(world: int, rank: int, dev, G: int, steps: int, warmup: int, M: int = 1, K: int = 4096,
+                n_total: int = 32000, wname: str = "q4_0") -> dict:
+    """BASELINE configs[4] as STRONG scaling: the N=32000 GEMV split over the ranks, both legs, and
+    the same GEMV on ONE GPU (this rank's own) in the same run as the denominator."""
+    wt = WTYPES[wname]
+    s0, s1 = shard_rows(n_total, world, rank)
+    rows = rows_per_rank(n_total, world)
+    a_h, b_h = qhost.fill_step4(M, n_total, K, 42, s0, s1)
+    aq = qg.quantize_q8_1(torch.from_numpy(a_h).to(dev))
+    bq = qg.quantize(torch.from_numpy(b_h).to(dev), wt)
+    del a_h, b_h
+    R = max(G, math.ceil(600e6 / max(bq.numel(), 1)))
+    wc = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
+    wc.copy_(bq.unsqueeze(0).expand_as(wc))
+    mods = [RowShardedW4A8(wc[i], n_total, K, wt) for i in range(R)]
+    legs = {form: sharded_leg(mods, aq, M, G, rows, world, steps, warmup, form, dev)
+            for form in ("per_launch", "batched")}
+    del mods, wc
+    torch.cuda.empty_cache()
+    one = measure_config(wname, M, n_total, K, dev, G, forms=("single", "batched"))
+    one_single = one[0]["us_per_launch"]
+    one_batched = one[1]["us_per_gemv"]
+    return {"config": f"{wname} M={M} N={n_total} K={K}: {rows} rows per GPU x {world} GPUs, all-gather per step of {G}",
+            "per_launch": legs["per_launch"], "batched": legs["batched"],
+            "one_gpu_n32000": {"single_us_per_launch": one_single, "batched_us_per_gemv": one_batched},
+            "strong_speedup_vs_1gpu_n32000": {
+                "per_launch": round(one_single / legs["per_launch"]["us_per_gemv"], 3),
+                "batched": round(one_batched / legs["batched"]["us_per_gemv"], 3),
+                "note": "1-GPU us per GEMV / N-GPU us per GEMV (wall clock per step incl. the all-gather, max over "
+                        "ranks), like for like per leg; DESIGN.md §7"}}
 
 
 def main() -> None:
@@ -203,7 +379,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the side measurements of BASELINE configs[2] and [3] (N = 1 only)")
+                    help="skip the side measurements of BASELINE configs[2], [3] and [4]-on-1-GPU (N = 1 only)")
+    ap.add_argument("--no-floor", action="store_true", help="skip the single-launch floor (roofline.floor_us)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling N=32000 legs")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -386,6 +564,21 @@ def main() -> None:
         if not torch.equal(bout[0, :, :local], outs[0][0, :, :local]):
             raise RuntimeError("batched GEMV differs from the single-launch GEMV")
 
+    # ---- the same G GEMVs as ONE pointer-array grouped launch (qg_gemm_w4a8_grouped, through the
+    #      shipped module's compute_local_group): independent weight / output pointers per item
+    grouped_us = None
+    if graphs is not None and args.algo == 0:
+        gout = torch.zeros((G, M, rows), dtype=torch.float32, device=dev)
+        grouped_us = graph_time_us(lambda: RowShardedW4A8.compute_local_group(mods[:G], aq, M, gout), 20, G)
+        if not torch.equal(gout[:, :, :local], outs[0][:, :, :local]):
+            raise RuntimeError("grouped GEMV differs from the single-launch GEMV")
+
+    # ---- the single-launch floor of this size under the same protocol (roofline.floor_us)
+    floor = None
+    if graphs is not None and not args.no_floor:
+        rpb = 16  # the M = 1 GEMV's rows per 1024-thread workgroup (qg_gemv.hip)
+        floor = measure_floor(dev, wcopies, G, algo_bytes(M, local, K, bb), (local + rpb - 1) // rpb, 1024)
+
     # ---- N > 1: the step's all-gather alone (same bytes, no GEMVs beside it), so the per-GPU kernel
     #      time and the gather latency are reported separately (SURVEY.md §7, 8-GPU hard part)
     gather_us = None
@@ -416,6 +609,12 @@ def main() -> None:
             g_hot.replay()
         torch.cuda.synchronize()
         hot_us = (time.perf_counter() - th) / (10 * G) * 1e6
+
+    strong = None
+    if world > 1 and not args.no_strong and graphs is not None:
+        del mods, wcopies
+        torch.cuda.empty_cache()
+        strong = strong_legs(world, rank, dev, G, args.steps, args.warmup)
 
     flops_per_gemv = 2.0 * M * n_total * K
     total_flops = flops_per_gemv * G * args.steps
@@ -455,13 +654,24 @@ def main() -> None:
                          "us_per_launch": round(launch_us, 3), "bytes_per_launch": launch_bytes,
                          "timing": "HIP events on the launch stream over the timed graph replays, "
                                    "per launch incl. its dispatch boundary",
-                         "per_step": step_pct},
+                         "per_step": step_pct,
+                         "floor_us": None if floor is None else floor["read_us"],
+                         "floor_frac": None if floor is None else round(launch_bytes / floor["read_us"] / 1e3 / HBM_PEAK_GBPS, 4),
+                         "floor": None if floor is None else dict(floor, note=(
+                             "single-launch floor, same protocol: empty kernel with the GEMV grid, and the fastest "
+                             "pure 16-B coalesced read of bytes_per_launch per launch over the same rotating copies "
+                             "(libqg_calib.so)"))},
             "batched": None if batched_us is None else {
                 "us_per_gemv": round(batched_us, 3),
                 "tflops": round(flops_per_gemv / world / batched_us / 1e6, 3),
                 "gbps": round(launch_bytes / batched_us / 1e3, 1),
                 "frac": round(launch_bytes / batched_us / 1e3 / HBM_PEAK_GBPS, 4),
                 "note": f"{G} GEMVs on distinct weight copies per qg_gemm_w4a8_strided_batched launch"},
+            "grouped": None if grouped_us is None else {
+                "us_per_gemv": round(grouped_us, 3),
+                "frac": round(launch_bytes / grouped_us / 1e3 / HBM_PEAK_GBPS, 4),
+                "note": f"{G} GEMVs on distinct weight copies per qg_gemm_w4a8_grouped launch (pointer array)"},
+            "strong": strong,
             "gather": None if gather_us is None else {
                 "us_per_step": round(gather_us, 2), "bytes_per_rank": G * M * rows * 4,
                 "note": f"all_gather_into_tensor of one step's {G} output slices alone ({backend})"},
@@ -469,18 +679,25 @@ def main() -> None:
                                                    "tflops": round(flops_per_gemv / world / hot_us / 1e6, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            one, mt = cpu_baseline(M, n_total, K, wtype, args.cpu_seconds)
-            out["cpu_baseline"] = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in one.items()}
-            out["cpu_baseline_mt"] = [{k: (round(v, 6) if isinstance(v, float) else v) for k, v in x.items()}
-                                      for x in mt]
+            one, twin, mt = cpu_baseline(M, n_total, K, wtype, args.cpu_seconds)
+            rnd = lambda d: {k: (round(v, 6) if isinstance(v, float) else v) for k, v in d.items()}
+            out["cpu_baseline"] = rnd(one)
+            out["cpu_baseline_twin"] = rnd(twin)
+            out["cpu_baseline_mt"] = [rnd(x) for x in mt]
         else:
             out["cpu_baseline"] = None
         if world == 1 and not args.no_configs and args.wtype == "q4_0" and args.n == 0 and args.m == 1 and args.k == 4096:
             # BASELINE configs[2] (the M=32 prefill) and configs[3] (all-quants GEMV), measured on the
             # same GPU in the same run (parity cases otherwise; not part of `value`)
             torch.cuda.empty_cache()
-            sides = [("q4_0", 32, 4096, 4096), ("q4_1", 1, 4096, 4096), ("q5_0", 1, 4096, 4096), ("q5_1", 1, 4096, 4096)]
-            out["side_configs"] = [measure_config(w, m_, n_, k_, dev) for (w, m_, n_, k_) in sides]
+            # plus configs[4]'s full N=32000 GEMV on this ONE GPU, single launches and one grouped launch
+            # of G: the denominators of the N>1 strong-scaling ratios
+            del mods, wcopies
+            torch.cuda.empty_cache()
+            sides = [("q4_0", 32, 4096, 4096, ("single",)), ("q4_1", 1, 4096, 4096, ("single",)),
+                     ("q5_0", 1, 4096, 4096, ("single",)), ("q5_1", 1, 4096, 4096, ("single",)),
+                     ("q4_0", 1, 32000, 4096, ("single", "batched"))]
+            out["side_configs"] = [r for (w, m_, n_, k_, f) in sides for r in measure_config(w, m_, n_, k_, dev, forms=f)]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

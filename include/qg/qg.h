@@ -2,7 +2,9 @@
  * qg/qg.h — C-ABI of the MI355X (gfx950) W4A8 quantized GEMM/GEMV library `libqg_hip.so`.
  *
  * Plain C: raw device pointers, sizes, an opaque HIP stream. Every call is stream-ordered and
- * asynchronous (no host sync), stateless and reentrant; the caller owns all buffers
+ * asynchronous (no host sync — the one exception is the one-time growth of a workspace the library
+ * keeps for a stream, see qg_gemm_w4a8_ws / qg_gemm_w4a16_ws, which the _ws forms avoid), reentrant;
+ * the caller owns all buffers
  * (destination-passing, schemas/docs/solution.md:27-42). Unlike the reference's `void` launch
  * wrappers (include/gemm_cuda_naive.cuh:285-292 — no error check), every entry point returns a
  * qg_status: 0 on success, a negative code otherwise; nothing is launched on a validation error.
@@ -81,6 +83,36 @@ int qg_gemm_w4a8_ldc(const void* A_q8_1, const void* B, float* C, int M, int N, 
 int qg_gemm_q4_0_q8_1_w4a8(const void* A_q8_1, const void* B_q4_0, float* C, int M, int N, int K,
                            qg_stream_t stream);
 
+/* As qg_gemm_w4a8 (QG_ALGO_AUTO) with a caller workspace for the odd-K/32 prefill route (K/32 not a
+ * multiple of 8, or 2-B aligned weights, at M >= 32 and N >= 1024): weights and activations are
+ * copied into zero-padded rows inside `workspace` (>= qg_gemm_w4a8_workspace_size(M, N, K, wtype)
+ * bytes, 256-B aligned; 0 for shapes that never take that route) and the MFMA kernel runs on the
+ * copy. Capture-safe (a graph keeps the caller's pointer). Without a workspace, qg_gemm_w4a8 uses
+ * a buffer the library keeps per (device, stream) — it grows to the largest N*K'/32*bb +
+ * M*K'/32*36 bytes seen on that stream (K' = K rounded up to 256), is held until
+ * qg_release_workspaces(), and growing it synchronizes that stream once; during stream capture
+ * that buffer is never used and such shapes run the ragged kernel instead (same results to the
+ * summation-order bound, not bit for bit). Weights used many times: repack once with
+ * qg_repack_weights and call qg_gemm_w4a8_prepacked. */
+size_t qg_gemm_w4a8_workspace_size(int M, int N, int K, int wtype);
+int qg_gemm_w4a8_ws(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
+                    size_t workspace_bytes, qg_stream_t stream);
+
+/* Load-time weight layout for K/32 not a multiple of 8 (e.g. K = 4128): rows of K'/32 blocks,
+ * K'/32 = round_up(K/32, 8), the real blocks first and then zero blocks (d = 0: every padded term is
+ * an exact +0 of the reference's sum). qg_repack_weights writes B_packed (16-B aligned,
+ * qg_repack_weights_bytes(N, K, wtype) bytes) from B [N][K/32]; one streaming kernel.
+ * qg_gemm_w4a8_prepacked then computes the SAME product as qg_gemm_w4a8(A, B, ...) (within the
+ * summation-order bound; K is the logical K) from B_packed: the activations are padded into
+ * `workspace` (>= qg_gemm_w4a8_prepacked_workspace_size(M, K) bytes, 16-B aligned; 0 when K/32 is
+ * already a multiple of 8) and the QG_ALGO_AUTO kernel runs on K' — no per-call weight copy.
+ * Capture-safe. */
+size_t qg_repack_weights_bytes(int N, int K, int wtype);
+int qg_repack_weights(const void* B, void* B_packed, int N, int K, int wtype, qg_stream_t stream);
+size_t qg_gemm_w4a8_prepacked_workspace_size(int M, int K);
+int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, int M, int N, int K, int wtype,
+                           void* workspace, size_t workspace_bytes, qg_stream_t stream);
+
 /* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
  * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of
  * gemm_w8a8_reference (include/gemm_reference.h:233-267). Same as qg_gemm_w4a8(..., QG_TYPE_Q8_0). */
@@ -121,6 +153,24 @@ int qg_gemm_q4_0_fp32(const void* weight_q4_0, const float* activation, float* o
  * One launch on the GEMV path (M <= 8), so the per-launch cost is paid once for the batch. */
 int qg_gemm_w4a8_strided_batched(const void* A_q8_1, int64_t strideA, const void* B, int64_t strideB, float* C,
                                  int64_t strideC, int batch, int M, int N, int K, int wtype, qg_stream_t stream);
+
+/* Grouped products with independent pointers and row counts (a decoder layer's Q / K / V or
+ * gate / up projections; the experts an MoE step selects): item i computes
+ * C_i[m * ldc_i + n] = A_i[M][K] . B_i[N_i][K]^T (ldc_i = 0 means N_i). One M, K and weight type for
+ * the group. Where QG_ALGO_AUTO picks the GEMV for every item (M <= 4 at aligned shapes), up to 64
+ * items go out in ONE launch (the descriptor travels in the kernel arguments: no device
+ * allocation, capture-safe, host `items` array read before return); otherwise the items are
+ * enqueued one by one. Either way each C_i is bit-identical to qg_gemm_w4a8_ldc(A_i, B_i, C_i, M,
+ * N_i, K, ldc_i, wtype, QG_ALGO_AUTO). Items with N_i == 0 are skipped. Replaces a host loop over
+ * gemm_q4_0_q8_1_warp-style launches (kernels/gemm/gemm_warp_optimized.cuh:933-1070). */
+typedef struct {
+    const void* A_q8_1;  /* block_q8_1 [M][K/32] (items may share it) */
+    const void* B;       /* weight blocks [N][K/32] of the group's wtype */
+    float* C;            /* [M][ldc] */
+    int N;
+    int ldc;             /* output row stride in floats, 0 = N */
+} qg_gemv_item;
+int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int wtype, qg_stream_t stream);
 
 /* ---- weight-major twins (kernels/gemm/gemm_quant_formats.cuh:343-428) ---------------------
  * out[M][N] = W[M][K/32] . A[N][K/32]^T, M = weight rows, N = tokens. */

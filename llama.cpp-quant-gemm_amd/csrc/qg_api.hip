@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <utility>
@@ -21,43 +22,63 @@ using namespace qg;
 
 namespace qg {
 namespace {
-std::mutex g_ws_mu;
+std::mutex g_ws_mu;  // guards the map; each entry has its own lock for its buffer
+struct WsEntry {
+    void* p = nullptr;
+    size_t n = 0;
+    std::mutex mu;
+};
 // key: (device, stream, slot) — slot 0 the W4A16 split-K workspace (its counters must stay zero
 // between calls), slot 1 the padded-repack buffers of the odd-K/32 prefill (qg_repack.hip)
-std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> g_ws;
+std::map<std::tuple<int, hipStream_t, int>, std::unique_ptr<WsEntry>> g_ws;
 }  // namespace
 
-void* stream_workspace(hipStream_t st, size_t bytes, int slot) {
+void* stream_workspace(hipStream_t st, size_t bytes, int slot, std::unique_lock<std::mutex>* hold) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     // Never hand the library's buffer to a stream capture: a graph would keep its raw pointer,
     // and a later eager call that grows the buffer (or qg_release_workspaces) would free it under
-    // the graph. Captured calls run without split-K; graphs pass their own workspace
+    // the graph. Captured calls run without it; graphs pass their own workspace
     // through the _ws entry points.
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
         (void)hipGetLastError();
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    auto& e = g_ws[std::make_tuple(dev, st, slot)];
-    if (e.first && e.second >= bytes) return e.first;
-    const size_t sz = std::max(bytes, (size_t)4 << 20);
-    void* p = nullptr;
-    if (hipMalloc(&p, sz) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
+    WsEntry* e;
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        auto& up = g_ws[std::make_tuple(dev, st, slot)];
+        if (!up) up.reset(new WsEntry);
+        e = up.get();
     }
-    if (hipMemsetAsync(p, 0, sz, st) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipFree(p);
-        return nullptr;
+    // The entry's lock is held while the buffer grows and, with `hold`, until the caller has
+    // enqueued every kernel that uses it (two host threads on one stream must not
+    // interleave a multi-kernel sequence on one buffer).
+    std::unique_lock<std::mutex> lk(e->mu);
+    if (!e->p || e->n < bytes) {
+        const size_t sz = std::max(bytes, (size_t)4 << 20);
+        void* p = nullptr;
+        if (hipMalloc(&p, sz) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        if (hipMemsetAsync(p, 0, sz, st) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(p);
+            return nullptr;
+        }
+        if (e->p) {
+            // launches still queued on st may use the old block: the one host sync of the library,
+            // once per growth (documented in qg.h; the _ws entry points never reach it)
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(e->p);
+        }
+        e->p = p;
+        e->n = sz;
     }
-    if (e.first) {
-        (void)hipStreamSynchronize(st);  // launches still queued on st may use the old block
-        (void)hipFree(e.first);
-    }
-    e = {p, sz};
+    void* p = e->p;
+    if (hold) *hold = std::move(lk);
     return p;
 }
 
@@ -71,11 +92,15 @@ void describe_kernel(const GemmArgs& g, const char* fmt, ...) {
 
 void release_workspaces() {
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (auto& kv : g_ws)
-        if (kv.second.first) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(kv.second.first);
+    bool synced = false;
+    for (auto& kv : g_ws) {
+        std::lock_guard<std::mutex> le(kv.second->mu);
+        if (kv.second->p) {
+            if (!synced) (void)hipDeviceSynchronize();
+            synced = true;
+            (void)hipFree(kv.second->p);
         }
+    }
     g_ws.clear();
 }
 }  // namespace qg
@@ -365,6 +390,118 @@ int qg_gemm_w4a8_strided_batched(const void* A, int64_t strideA, const void* B, 
     g.ldc_m = N; g.ldc_n = 1;
     g.batch = batch; g.sA = strideA; g.sB = strideB; g.sC = strideC;
     return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)stream);
+}
+
+size_t qg_gemm_w4a8_workspace_size(int M, int N, int K, int wtype) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 32 != 0 || !is_weight_type(wtype)) return 0;
+    GemmArgs g;
+    g.A = (const void*)256; g.B = (const void*)256; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    return repack_eligible(g) ? repack_workspace_bytes(g) : 0;
+}
+
+int qg_gemm_w4a8_ws(const void* A, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
+                    size_t workspace_bytes, qg_stream_t stream) {
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.ws = workspace; g.ws_bytes = workspace_bytes;
+    return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)stream);
+}
+
+size_t qg_repack_weights_bytes(int N, int K, int wtype) {
+    if (N < 0 || K <= 0 || K % 32 != 0 || !is_weight_type(wtype)) return 0;
+    return (size_t)N * (size_t)padded_blocks(K) * (size_t)block_bytes(wtype);
+}
+
+int qg_repack_weights(const void* B, void* B_packed, int N, int K, int wtype, qg_stream_t stream) {
+    if (N < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(wtype)) return QG_ERR_UNSUPPORTED;
+    if (N == 0) return QG_OK;
+    if (!B || !B_packed) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)B & 1) != 0 || ((uintptr_t)B_packed & 15) != 0) return QG_ERR_ALIGN;
+    const int bb = block_bytes(wtype);
+    return hip_status(launch_pad_rows(B, B_packed, N, (K / 32) * bb, padded_blocks(K) * bb, (hipStream_t)stream));
+}
+
+size_t qg_gemm_w4a8_prepacked_workspace_size(int M, int K) {
+    if (M <= 0 || K <= 0 || K % 32 != 0 || padded_blocks(K) == K / 32) return 0;
+    return (size_t)M * (size_t)padded_blocks(K) * 36;
+}
+
+int qg_gemm_w4a8_prepacked(const void* A, const void* B_packed, float* C, int M, int N, int K, int wtype,
+                           void* workspace, size_t workspace_bytes, qg_stream_t stream) {
+    if (M < 0 || N < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(wtype)) return QG_ERR_UNSUPPORTED;
+    if (M == 0 || N == 0) return QG_OK;
+    if (!A || !B_packed || !C) return QG_ERR_INVALID_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    const int nbp = padded_blocks(K);
+    GemmArgs g;
+    g.A = A; g.B = B_packed; g.C = C; g.M = M; g.N = N; g.K = nbp * 32; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    if (nbp != K / 32) {  // activations padded into the caller's workspace, same zero blocks
+        if (!workspace || workspace_bytes < qg_gemm_w4a8_prepacked_workspace_size(M, K)) return QG_ERR_INVALID_ARG;
+        if (((uintptr_t)A & 1) != 0 || ((uintptr_t)workspace & 15) != 0) return QG_ERR_ALIGN;
+        const hipError_t e = launch_pad_rows(A, workspace, M, (K / 32) * 36, nbp * 36, st);
+        if (e != hipSuccess) return hip_status(e);
+        g.A = workspace;
+    }
+    return run_gemm(g, QG_ALGO_AUTO, st);
+}
+
+int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int wtype, qg_stream_t stream) {
+    if (count < 0 || M < 0 || (count > 0 && !items)) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(wtype)) return QG_ERR_UNSUPPORTED;
+    const hipStream_t st = (hipStream_t)stream;
+    auto item_args = [&](const qg_gemv_item& it) {
+        GemmArgs g;
+        g.A = it.A_q8_1; g.B = it.B; g.C = it.C; g.M = M; g.N = it.N; g.K = K; g.wtype = wtype;
+        g.ldc_m = it.ldc ? it.ldc : it.N; g.ldc_n = 1;
+        return g;
+    };
+    // validate every item before anything is enqueued; one launch only if AUTO picks the GEMV for all
+    bool one_launch = M > 0;
+    for (int i = 0; i < count; ++i) {
+        const qg_gemv_item& it = items[i];
+        if (it.N < 0 || it.ldc < 0 || (it.ldc != 0 && it.ldc < it.N)) return QG_ERR_INVALID_ARG;
+        if (it.N == 0 || M == 0) continue;
+        if (!it.A_q8_1 || !it.B || !it.C) return QG_ERR_INVALID_ARG;
+        if (((uintptr_t)it.B & 1) != 0) return QG_ERR_ALIGN;
+        const GemmArgs g = item_args(it);
+        one_launch = one_launch && select_algo(g) == QG_ALGO_GEMV && gemv_eligible(g);
+    }
+    if (M == 0) return QG_OK;
+    if (!one_launch) {
+        for (int i = 0; i < count; ++i) {
+            if (items[i].N == 0) continue;
+            GemmArgs g = item_args(items[i]);
+            const int rc = run_gemm(g, QG_ALGO_AUTO, st);
+            if (rc != QG_OK) return rc;
+        }
+        return QG_OK;
+    }
+    for (int i0 = 0; i0 < count;) {
+        GemvGroup grp = {};
+        grp.M = M; grp.K = K;
+        int maxn = 0;
+        for (; i0 < count && grp.count < GEMV_GROUP_MAX; ++i0) {
+            const qg_gemv_item& it = items[i0];
+            if (it.N == 0) continue;
+            grp.it[grp.count++] = GemvItemDesc{it.A_q8_1, it.B, it.C, it.N, it.ldc ? it.ldc : it.N};
+            maxn = std::max(maxn, it.N);
+        }
+        if (grp.count == 0) break;
+        GemmArgs g;
+        g.A = grp.it[0].A; g.B = grp.it[0].B; g.C = grp.it[0].C; g.M = M; g.N = maxn; g.K = K; g.wtype = wtype;
+        g.ldc_m = grp.it[0].ldc; g.ldc_n = 1;
+        g.group = &grp;
+        const int rc = hip_status(launch_gemv(g, st));
+        if (rc != QG_OK) return rc;
+    }
+    return QG_OK;
 }
 
 int qg_gemm_w4a8(const void* A, const void* B, float* C, int M, int N, int K, int wtype, qg_stream_t stream) {

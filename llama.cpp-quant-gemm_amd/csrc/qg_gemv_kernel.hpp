@@ -229,7 +229,7 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
-                                          int32_t* __restrict__ sumi_out) {
+                                          int32_t* __restrict__ sumi_out, int tile_in = -1) {
     using G = gemv_geom<F, BPL>;
     QG_STAMP(t0);
     QG_CLK(c0);
@@ -251,7 +251,8 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     // end-of-kernel write-back is the GEMV's largest fixed cost after the launch;
     // profiles/r02_tuning/ab_xcd.txt: M=1 3.33 -> 3.29 us, M=2 3.66 -> 3.58). Larger grids keep
     // the linear order (N=32000: 12.55 us linear, 13.28 remapped).
-    const int tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    // (a grouped launch passes the workgroup's tile within its item, tile_in >= 0)
+    const int tile = tile_in >= 0 ? tile_in : gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int row = tile * RPB + (tid >> 6) * RPW + lane / LPR;
     const bool row_ok = row < N;
 
@@ -441,6 +442,26 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 
+// Grouped GEMV (qg_gemm_w4a8_grouped): up to GEMV_GROUP_MAX independent products with their own A,
+// B, C and N (and output row stride), one M and K, in ONE launch — e.g. a decoder layer's Q / K / V
+// or gate / up projections. The descriptor travels by value in the kernel arguments (GemvGroup in
+// qg_kernels.hpp: no device allocation, capture-safe); blockIdx.y is the item, blockIdx.x its row
+// tile, and workgroups past an item's rows exit at once (grid.x = the largest item's tiles). The
+// item's pointers are ONE scalar load (32-B record); the outputs are bit-identical to the single
+// launch (same body, same per-row summation). A first version located each workgroup's item in a
+// tile prefix table (a lane-parallel vector load + ballot, or 64 scalar compares): 1.72 / 2.10 us per
+// GEMV in a group of 64 vs 1.44 for the strided batch (the lookup sat in front of every workgroup's
+// weight stream).
+template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU>
+__global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
+    constexpr int RPB = (WGS / 64) * (64 / LPR);
+    const GemvItemDesc d = grp.it[blockIdx.y];
+    if ((int)blockIdx.x * RPB >= d.N) return;  // past this item's rows (uniform)
+    gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, 0>(
+        reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K, d.C, 0,
+        d.ldc, 1, nullptr, (int)blockIdx.x);
+}
+
 // Host side -------------------------------------------------------------------------------------
 
 template <int F, int BPL> inline size_t gemv_lds_bytes(int M, int K) {
@@ -475,6 +496,21 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                         m1 ? "m1" : (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) ? "short" : "full", grid,
                         g.batch);
         return hipSuccess;
+    }
+    if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT) {
+        if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
+            const GemvGroup& grp = *static_cast<const GemvGroup*>(g.group);
+            int tiles = 0;
+            for (int i = 0; i < grp.count; ++i) tiles = std::max(tiles, (grp.it[i].N + RPB - 1) / RPB);
+            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true> : gemvg_kernel<F, MT, BPL, LPR, WGS, PRE && (MT <= 2), false>;
+            if (lds > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            if (tiles == 0 || grp.count == 0) return hipSuccess;
+            hipLaunchKernelGGL(kg, dim3(tiles, grp.count), dim3(WGS), lds, st, grp);
+            return hipGetLastError();
+        }
     }
     if (m1) {
         auto k1 = one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;

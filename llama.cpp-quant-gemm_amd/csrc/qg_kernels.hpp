@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
+
 namespace qg {
 
 // Activation input of a product: Q8_1 blocks, or FP32 / FP16 rows quantized inside the kernel.
@@ -23,9 +26,37 @@ struct GemmArgs {
     long sA = 0, sB = 0, sC = 0; // batch strides: bytes, bytes, floats
     void* ws = nullptr;          // optional device workspace (split-K partials + tile counters)
     size_t ws_bytes = 0;
+    const void* group = nullptr; // GEMV path: a GemvGroup descriptor (qg_gemm_w4a8_grouped); M, K, wtype
+                                 // shared, N = the largest item's
     char* describe = nullptr;    // qg_debug_config: the leaf launcher writes the kernel it would
     size_t describe_len = 0;     // launch here (family + template parameters) and launches nothing
 };
+
+// Descriptor of a grouped GEMV launch (qg_gemm_w4a8_grouped), passed by value as the kernel argument.
+constexpr int GEMV_GROUP_MAX = 64;
+struct GemvItemDesc {  // 32 B: one s_load_dwordx8 in the kernel
+    const void* A;
+    const void* B;
+    float* C;
+    int N, ldc;
+};
+struct GemvGroup {
+    int count, M, K, pad;
+    GemvItemDesc it[GEMV_GROUP_MAX];
+};
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel instantiation, device): `done`
+// is that instantiation's atomic device bitmask (a process may drive several GPUs from
+// several threads; the attribute is per device). Not a stream operation, so capture-safe.
+inline hipError_t set_max_lds_once(const void* fn, int bytes, std::atomic<unsigned long long>& done) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    const unsigned long long bit = dev < 64 ? 1ull << dev : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 // printf-style description of a kernel instantiation into g.describe (qg_debug_config). SUMI is
 // deliberately not part of it: the parity hook must name the product's kernel.
@@ -55,8 +86,14 @@ hipError_t launch_ragged(const GemmArgs& g, hipStream_t st);
 // computes at any aligned K; the sumi hook runs the same MFMA instantiation into a padded image and
 // compacts it. repack_eligible: shape rules only (pointers not needed).
 bool repack_eligible(const GemmArgs& g);
-// returns hipErrorNotReady (nothing enqueued) when no workspace can be had right now (e.g. capture)
+// returns hipErrorNotReady (nothing enqueued) when no workspace can be had right now (e.g. capture
+// without a caller workspace g.ws of >= repack_workspace_bytes(g))
 hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st);
+size_t repack_workspace_bytes(const GemmArgs& g);  // weights + activations (+ the sumi image)
+// Weights [N][K/32] -> rows of K'/32 = round_up(K/32, 8) blocks, zero blocks after the real ones
+// (qg_repack_weights); activations the same (qg_gemm_w4a8_prepacked). Both enqueue one kernel.
+int padded_blocks(int K);
+hipError_t launch_pad_rows(const void* src, void* dst, long rows, int row_bytes, int padded_row_bytes, hipStream_t st);
 
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.
 // g.ws / g.ws_bytes: optional caller workspace for the split-K prefill (>= w16_workspace_bytes,
@@ -72,7 +109,8 @@ hipError_t launch_fp32(const GemmArgs& g, hipStream_t st);
 // one stream are ordered, and every split-K launch leaves its counters zero). nullptr when it
 // cannot be allocated right now (e.g. the stream is being captured): callers fall back to a
 // kernel without a workspace.
-void* stream_workspace(hipStream_t st, size_t bytes, int slot = 0);
+// hold: keep the buffer's lock until the caller has enqueued everything that uses it.
+void* stream_workspace(hipStream_t st, size_t bytes, int slot = 0, std::unique_lock<std::mutex>* hold = nullptr);
 
 // Quantizers / dequantizers (one thread per 32-element block, reference rounding semantics).
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);

@@ -800,12 +800,9 @@ hipError_t mmq_launch(const GemmArgs& g, hipStream_t st) {
         auto k1 = mmq1_kernel<F, BN, TT, W, SUMI, P16, NB, SB, EPI2, OPT>;
         const size_t lds = G::dyn_lds(g.K / QK / SB);
         if (lds > 64 * 1024) {
-            static bool attr1_set = false;  // once per instantiation (not a stream op: capture-safe)
-            if (!attr1_set) {
-                hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                if (e != hipSuccess) return e;
-                attr1_set = true;
-            }
+            static std::atomic<unsigned long long> attr_done{0};
+            const hipError_t e = set_max_lds_once((const void*)k1, 160 * 1024, attr_done);
+            if (e != hipSuccess) return e;
         }
         void* out = SUMI ? (void*)g.sumi : (void*)g.C;
         hipLaunchKernelGGL(k1, grid, dim3(W * 64), lds, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.M, g.N, g.K, out,
@@ -824,12 +821,9 @@ hipError_t mmq_launch_full(const GemmArgs& g, hipStream_t st, dim3 grid) {
     float* part = KS > 1 ? (float*)((uint8_t*)g.ws + ((((size_t)grid.x * grid.y) * 4 + 255) & ~(size_t)255)) : nullptr;
     const size_t lds = G::dyn_lds(g.K / QK / SB / KS);
     if (lds > 64 * 1024) {
-        static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
-        if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-            attr_set = true;
-        }
+        static std::atomic<unsigned long long> attr_done{0};
+        const hipError_t e = set_max_lds_once((const void*)k, 160 * 1024, attr_done);
+        if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k, grid, dim3(W * 64), lds, st, (const uint8_t*)g.A, (const uint8_t*)g.B, g.C, g.sumi, g.M,
                        g.N, g.K, g.ldc_m, g.ldc_n, part, cnt);

@@ -93,19 +93,44 @@ bool repack_eligible(const GemmArgs& g) {
     return mfma_eligible(g2);
 }
 
+int padded_blocks(int K) { return (K / QK + PADB - 1) / PADB * PADB; }
+
+size_t repack_workspace_bytes(const GemmArgs& g) {
+    const int nbp = padded_blocks(g.K);
+    const long wimg = round256((long)g.N * nbp * wbytes(g.wtype)), aimg = round256((long)g.M * nbp * Q8_1_BYTES);
+    const long simg = g.sumi ? round256((long)g.M * g.N * nbp * 4) : 0;
+    return (size_t)(wimg + aimg + simg);
+}
+
+hipError_t launch_pad_rows(const void* src, void* dst, long rows, int rb, int rbp, hipStream_t st) {
+    const long words = rows * rbp / 8;
+    const long blocks = (words + 255) / 256;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(repack_pad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<const uint16_t*>(src),
+                       static_cast<uint64_t*>(dst), words, rb, rbp, static_cast<const uint16_t*>(nullptr),
+                       static_cast<uint64_t*>(nullptr), 0L, 0, 8);
+    return hipGetLastError();
+}
+
 hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st) {
     GemmArgs g2 = padded(g);
     const int nb = g.K / QK, nbp = g2.K / QK;
     const int rb = nb * wbytes(g.wtype), rbp = nbp * wbytes(g.wtype);
     const int ab = nb * Q8_1_BYTES, abp = nbp * Q8_1_BYTES;
     const long wimg = round256((long)g.N * rbp), aimg = round256((long)g.M * abp);
-    const long simg = g.sumi ? round256((long)g.M * g.N * nbp * 4) : 0;
     if (g.describe) {  // configuration query: the MFMA instantiation this call would run
         g2.A = reinterpret_cast<const void*>(256);
         g2.B = reinterpret_cast<const void*>(256);
         return launch_mfma(g2, st);
     }
-    uint8_t* ws = static_cast<uint8_t*>(stream_workspace(st, (size_t)(wimg + aimg + simg), 1));
+    // the caller's workspace (qg_gemm_w4a8_ws: capture-safe), else the library's per-stream one,
+    // its lock held until the last kernel below is enqueued
+    const size_t need = repack_workspace_bytes(g);
+    std::unique_lock<std::mutex> hold;
+    uint8_t* ws = nullptr;
+    if (g.ws && g.ws_bytes >= need && ((uintptr_t)g.ws & 255) == 0) ws = static_cast<uint8_t*>(g.ws);
+    else ws = static_cast<uint8_t*>(stream_workspace(st, need, 1, &hold));
     if (!ws) return hipErrorNotReady;
     const long wwords = (long)g.N * rbp / 8, awords = (long)g.M * abp / 8;
     const long blocks = (wwords + awords + 255) / 256;
@@ -117,6 +142,8 @@ hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st) {
     if (e != hipSuccess) return e;
     g2.B = ws;
     g2.A = ws + wimg;
+    g2.ws = nullptr;
+    g2.ws_bytes = 0;
     if (g.sumi) g2.sumi = reinterpret_cast<int32_t*>(ws + wimg + aimg);
     e = launch_mfma(g2, st);
     if (e != hipSuccess || !g.sumi) return e;

@@ -1177,11 +1177,10 @@ template <int F, int TT> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_
     float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
     constexpr size_t lds = (size_t)W16S_R * G::SBYTES + G::PLB;
     static_assert(lds <= 160 * 1024, "LDS per workgroup");
-    static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)w16s_kernel<TT, W16S_R, 0, F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    static std::atomic<unsigned long long> attr_done{0};
+    {
+        const hipError_t e = set_max_lds_once((const void*)w16s_kernel<TT, W16S_R, 0, F>, (int)lds, attr_done);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
     hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0, F>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
                        (const uint8_t*)g.B, g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n, p.ns, part, cnt);
@@ -1199,12 +1198,9 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
     constexpr size_t lds = (size_t)TT * KB * 3 * 1024;
     auto kfn = w16_sk_kernel<F, RT, TT, KB>;
     if (lds > 64 * 1024) {
-        static bool attr_set = false;  // once per instantiation (not a stream op: capture-safe)
-        if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            attr_set = true;
-        }
+        static std::atomic<unsigned long long> attr_done{0};
+        const hipError_t e = set_max_lds_once((const void*)kfn, (int)lds, attr_done);
+        if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(kfn, dim3(p.gx, p.gy, ks), dim3(RT * 64), lds, st, (const float*)g.A, (const uint8_t*)g.B, g.C,
                        g.M, g.N, g.K, g.ldc_m, g.ldc_n, g.K / QK / ks, part, cnt);

@@ -3,8 +3,8 @@
 // float operation is the single IEEE rounding the reference's scalar loops perform.
 //
 // Layout: a weight format is a traits struct (block bytes, field offsets, per-block formula); the
-// GEMM walks output rows (optionally over std::threads — each output's summation stays serial in
-// block order, so the thread count never changes a bit). Half <-> float goes through the F16C
+// GEMM walks output rows (optionally over a persistent worker pool — each output's summation stays
+// serial in block order, so the thread count never changes a bit). Half <-> float goes through the F16C
 // conversion instructions (round-to-nearest-even, as cuda_fp16's __float2half).
 #include <immintrin.h>
 #include <stdlib.h>
@@ -12,6 +12,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -90,12 +94,11 @@ struct FmtQ8_0 {
 };
 
 template <class F> inline int32_t block_sumi(const uint8_t* w, const ActBlock& a) {
-    // element pairs (k, k + 16) in the reference's loop order (integer sums are order-free anyway)
+    // element pairs (k, k + 16) in the reference's loop order (integer sums are order-free anyway);
+    // constant indices, so the per-format branches fold away
     int32_t sumi = 0;
-    for (int k = 0; k < QK / 2; ++k) {
-        sumi += (int32_t)a.qs[k] * F::value(w, k);
-        sumi += (int32_t)a.qs[k + QK / 2] * F::value(w, k + QK / 2);
-    }
+    for (int k = 0; k < QK / 2; ++k)
+        sumi += (int32_t)a.qs[k] * F::value(w, k) + (int32_t)a.qs[k + QK / 2] * F::value(w, k + QK / 2);
     return sumi;
 }
 
@@ -114,19 +117,86 @@ template <class F> void gemm_rows(const uint8_t* A, const uint8_t* B, float* C, 
         }
 }
 
+// Process-wide persistent worker pool: threads are started once (grown on demand) and parked on
+// a condition variable between jobs, so a multi-threaded call costs one wake-up per worker instead
+// of a thread start and join (which dominated a 1-9 ms GEMV at 256 threads). One job at a time
+// (callers are serialised by run_mu); the calling thread takes part 0.
+class Pool {
+  public:
+    static Pool& get() {
+        static Pool p;
+        return p;
+    }
+    void run(int parts, const std::function<void(int)>& fn) {
+        std::lock_guard<std::mutex> serial(run_mu_);
+        grow(parts - 1);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &fn;
+            parts_ = parts;
+            pending_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void grow(int n) {
+        while ((int)workers_.size() < n) {
+            const int id = (int)workers_.size() + 1;  // part index this worker takes
+            workers_.emplace_back([this, id] { loop(id); });
+        }
+    }
+    void loop(int id) {
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= parts_) continue;  // not needed for this job
+                job = job_;
+            }
+            (*job)(id);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* job_ = nullptr;
+    int parts_ = 0, pending_ = 0;
+    unsigned long long gen_ = 0;
+    bool stop_ = false;
+};
+
 template <class F> void gemm_threads(const void* A, const void* B, float* C, int M, int N, int K, int threads) {
     auto run = [&](int j0, int j1) {
         gemm_rows<F>((const uint8_t*)A, (const uint8_t*)B, C, M, N, K, j0, j1);
     };
     threads = std::max(1, std::min(threads, N));
     if (threads == 1) return run(0, N);
-    std::vector<std::thread> pool;
     const int per = (N + threads - 1) / threads;
-    for (int t = 0; t < threads; ++t) {
+    const std::function<void(int)> part = [&](int t) {
         const int j0 = t * per, j1 = std::min(N, j0 + per);
-        if (j0 < j1) pool.emplace_back(run, j0, j1);
-    }
-    for (auto& th : pool) th.join();
+        if (j0 < j1) run(j0, j1);
+    };
+    Pool::get().run(threads, part);
 }
 
 int check_gemm(const void* A, const void* B, const float* C, int M, int N, int K) {

@@ -162,6 +162,81 @@ def gemm_w4a8_batched(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int
     return out
 
 
+class _GemvItem(ctypes.Structure):
+    _fields_ = [("A_q8_1", ctypes.c_void_p), ("B", ctypes.c_void_p), ("C", ctypes.c_void_p),
+                ("N", ctypes.c_int), ("ldc", ctypes.c_int)]
+
+
+def gemm_w4a8_grouped(activations_q, weights_q, Ns, M: int, K: int, wtype: int = Q4_0, outs=None):
+    """Grouped activation-major products with independent pointers and row counts
+    (qg_gemm_w4a8_grouped): item i = activations_q[i] [M, K/32, 36] (items may share one tensor) x
+    weights_q[i] [Ns[i], K/32, bb] -> outs[i] [M, Ns[i]] (allocated unless given; a given out may be
+    a row-strided view, e.g. a column slice of a wider buffer). One launch for up to 64 items on the
+    GEMV path; each output bit-identical to gemm_w4a8 on its item."""
+    n = len(weights_q)
+    _require(len(activations_q) == n and len(Ns) == n, "item count mismatch")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    bb = BLOCK_BYTES[wtype]
+    items = (_GemvItem * max(n, 1))()
+    res, keep = [], []
+    dev = weights_q[0].device if n else torch.device("cuda")
+    for i in range(n):
+        a, w, N = activations_q[i], weights_q[i], int(Ns[i])
+        _require(a.is_cuda and w.is_cuda, "Inputs must be CUDA tensors")
+        _require(a.dtype == torch.uint8 and w.dtype == torch.uint8, "Inputs must be uint8")
+        _require(a.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+        _require(w.numel() == N * (K // 32) * bb, "Weight shape mismatch")
+        a, w = a.contiguous(), w.contiguous()
+        if outs is None:
+            o = torch.empty((M, N), dtype=torch.float32, device=w.device)
+        else:
+            o = outs[i]
+            _require(o.dtype == torch.float32 and o.shape == (M, N) and (N <= 1 or o.stride(1) == 1),
+                     "out must be float32 [M, N] with unit column stride")
+        keep += [a, w]
+        ldc = o.stride(0) if M > 1 else N
+        items[i] = _GemvItem(a.data_ptr(), w.data_ptr(), o.data_ptr(), N, ldc)
+        res.append(o)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.load().qg_gemm_w4a8_grouped(items, n, M, K, wtype, _stream(dev)), "gemm_w4a8_grouped")
+    return res
+
+
+def repack_weights(weight_q: torch.Tensor, N: int, K: int, wtype: int = Q4_0) -> torch.Tensor:
+    """Load-time layout for K/32 not a multiple of 8 (qg_repack_weights): [N, K'/32, bb] uint8,
+    the real blocks then zero blocks (K'/32 = round_up(K/32, 8)). Feed it to gemm_w4a8_prepacked."""
+    _require(weight_q.is_cuda and weight_q.dtype == torch.uint8, "weight_q must be a CUDA uint8 tensor")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    bb = BLOCK_BYTES[wtype]
+    _require(weight_q.numel() == N * (K // 32) * bb, "Weight shape mismatch")
+    lib = _lib.load()
+    nbytes = lib.qg_repack_weights_bytes(N, K, wtype)
+    out = torch.empty((N, nbytes // max(N * bb, 1), bb), dtype=torch.uint8, device=weight_q.device)
+    w = weight_q.contiguous()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.qg_repack_weights(_ptr(w), _ptr(out), N, K, wtype, _stream(w.device)), "repack_weights")
+    return out
+
+
+def gemm_w4a8_prepacked(activation_q: torch.Tensor, weight_packed: torch.Tensor, M: int, N: int, K: int,
+                        wtype: int = Q4_0) -> torch.Tensor:
+    """C [M, N] = the same product as gemm_w4a8(activation_q, weight_q, ...) from
+    repack_weights(weight_q) (qg_gemm_w4a8_prepacked; K is the logical K)."""
+    _require(activation_q.is_cuda and weight_packed.is_cuda, "Inputs must be CUDA tensors")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(activation_q.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    lib = _lib.load()
+    _require(weight_packed.numel() == lib.qg_repack_weights_bytes(N, K, wtype), "Packed weight shape mismatch")
+    a = activation_q.contiguous()
+    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    wsb = lib.qg_gemm_w4a8_prepacked_workspace_size(M, K)
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=a.device)
+    with torch.cuda.device(a.device):
+        _lib.check(lib.qg_gemm_w4a8_prepacked(_ptr(a), _ptr(weight_packed), _ptr(out), M, N, K, wtype, _ptr(ws), wsb,
+                                              _stream(a.device)), "gemm_w4a8_prepacked")
+    return out
+
+
 def _gemm_weight_major(sym: str, wtype: int, weight_q, activation_q, M, N, K):
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
     _check_blocks(weight_q, "Weight", M, K, BLOCK_BYTES[wtype])

@@ -29,6 +29,13 @@ SIGNATURES = {
     "qg_gemm_w4a8_ldc": ([P, P, P, I, I, I, I64, I, I, P], I),
     "qg_debug_config": ([I, I, I, I, I, I, ctypes.c_char_p, SZ], I),
     "qg_gemm_w4a8_strided_batched": ([P, I64, P, I64, P, I64, I, I, I, I, I, P], I),
+    "qg_gemm_w4a8_grouped": ([P, I, I, I, I, P], I),
+    "qg_gemm_w4a8_workspace_size": ([I, I, I, I], SZ),
+    "qg_gemm_w4a8_ws": ([P, P, P, I, I, I, I, P, SZ, P], I),
+    "qg_repack_weights_bytes": ([I, I, I], SZ),
+    "qg_repack_weights": ([P, P, I, I, I, P], I),
+    "qg_gemm_w4a8_prepacked_workspace_size": ([I, I], SZ),
+    "qg_gemm_w4a8_prepacked": ([P, P, P, I, I, I, I, P, SZ, P], I),
     "qg_gemm_q4_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_0_q8_1": ([P, P, P, I, I, I, P], I),

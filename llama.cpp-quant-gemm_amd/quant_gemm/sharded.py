@@ -51,6 +51,7 @@ class RowShardedW4A8:
         if weight_q_local.shape[0] != local:
             raise RuntimeError(f"rank {self.rank}: expected {local} weight rows, got {weight_q_local.shape[0]}")
         self.weight = weight_q_local
+        self._default = compute is None
         if compute is None:
             import quant_gemm
 
@@ -72,6 +73,25 @@ class RowShardedW4A8:
         if local > 0:
             self.compute(act_q, self.weight, M, local, self.K, out[:, :local] if local < self.rows else out)
         return out
+
+    @staticmethod
+    def compute_local_group(mods: "list[RowShardedW4A8]", act_q: torch.Tensor, M: int, outs: torch.Tensor) -> torch.Tensor:
+        """outs[i] = mods[i].compute_local(act_q, M, outs[i]) for several sharded products of one K
+        and weight type on this rank (e.g. a batch of independent projections sharing the
+        activations): with the default HIP compute, ONE grouped launch (qg_gemm_w4a8_grouped,
+        bit-identical outputs) instead of one launch per product; an injected compute runs them in
+        turn. outs: [len(mods), M, rows]."""
+        if not all(m._default and m.K == mods[0].K and m.wtype == mods[0].wtype and m.start == mods[0].start
+                   and m.stop == mods[0].stop for m in mods):
+            for m, o in zip(mods, outs):
+                m.compute_local(act_q, M, o)
+            return outs
+        import quant_gemm
+        local = mods[0].stop - mods[0].start
+        if local > 0:
+            quant_gemm.gemm_w4a8_grouped([act_q] * len(mods), [m.weight for m in mods], [local] * len(mods), M,
+                                         mods[0].K, mods[0].wtype, outs=[o[:, :local] for o in outs])
+        return outs
 
     def gather(self, out: torch.Tensor, gathered: torch.Tensor, async_op: bool = False):
         """One all-gather of every rank's ``out`` (any leading dims, e.g. [G, M, rows] for G

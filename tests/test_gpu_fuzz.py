@@ -43,6 +43,43 @@ def test_w4a8_random_shapes(O, qg, i, m, n, k, t):
     close_to_oracle(O, c, aq, bq, t, mfma=qg.select_algo(m, n, k, t) == 2)
 
 
+def repack_cases(n_cases=10, seed=4242):
+    """random odd K/32 (and K/32 % 8 != 0) at prefill sizes — the repack + MFMA route."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_cases):
+        m = int(rng.choice([32, 33, 40, 48, 64, 65, 96]))
+        n = int(rng.integers(1024, 2300))
+        nb = int(rng.integers(3, 140))
+        nb = nb | 1 if i % 2 == 0 else (nb // 2) * 2 + (2 if (nb // 2 * 2) % 8 == 0 else 0)
+        out.append((i, m, n, 32 * nb, FMTS[i % len(FMTS)]))
+    return out
+
+
+@pytest.mark.parametrize("i,m,n,k,t", repack_cases())
+def test_w4a8_random_repack_shapes(O, qg, i, m, n, k, t):
+    """Outputs within the reassociation bound and the parity hook's int32 sumi bit-exact through the
+    product instantiation (the padded-image MFMA kernel, compacted)."""
+    rng = np.random.default_rng(2000 + i)
+    aq, bq = random_blocks(rng, m, n, k, t)
+    assert qg.select_algo(m, n, k, t) == 2
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t))
+    close_to_oracle(O, c, aq, bq, t, mfma=True)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t))
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("i,m,n,k,t", w4a8_cases()[::4])
+def test_w4a8_random_shapes_sumi(O, qg, i, m, n, k, t):
+    """The parity hook on the sweep's shapes: int32 sumi bit-exact from the product instantiation."""
+    rng = np.random.default_rng(3000 + i)
+    aq, bq = random_blocks(rng, m, n, k, t)
+    got = host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t))
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("i", range(8))
 def test_w4a8_random_shapes_strided_out(O, qg, i):
     """Output rows in a column slice of a wider buffer (qg_gemm_w4a8_ldc), random shapes."""
