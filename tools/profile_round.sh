@@ -7,8 +7,8 @@ set -e
 OUT=gpurun_out/prof_round
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 20 --warmup 5"
-timeout -k 10 300 $B > $OUT/bench.json 2> $OUT/bench.err
+B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline"
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1
 # the same trace with dispatches serialised by one harmless counter (the plain trace pass slows each
 # dispatch of a 3.3 us kernel)
