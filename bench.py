@@ -103,6 +103,9 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     ref = a.double() @ b.double().T
     nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
     del a, b, ref, c
+    if "prepacked" in forms or "padded" in forms:  # the load-time layout for K/32 % 8 != 0 (qg_repack_weights)
+        bq = qg.repack_weights(bq, N, K, wt)
+        ap = qg.quantize_q8_1_padded(torch.from_numpy(qhost.fill_step4(M, N, K, 42, 0, 0)[0]).to(dev))
     R = max(G, math.ceil(600e6 / bq.numel()))
     copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
     copies.copy_(bq.unsqueeze(0).expand_as(copies))
@@ -114,6 +117,27 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
             def step() -> None:
                 for j in range(G):
                     qg.gemm_w4a8(aq, copies[j], M, N, K, wt, out=out[j])
+        elif form == "prepacked":
+            lib = qg._lib.load()
+            wsb = lib.qg_gemm_w4a8_prepacked_workspace_size(M, K)
+            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+
+            def step() -> None:
+                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_gemm_w4a8_prepacked(ctypes.c_void_p(aq.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                                  ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt,
+                                                  ctypes.c_void_p(ws.data_ptr()), wsb, cs) != 0:
+                        raise RuntimeError("qg_gemm_w4a8_prepacked failed")
+        elif form == "padded":
+            lib = qg._lib.load()
+
+            def step() -> None:
+                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_gemm_w4a8_padded(ctypes.c_void_p(ap.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                               ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt, cs) != 0:
+                        raise RuntimeError("qg_gemm_w4a8_padded failed")
         else:
             def step() -> None:
                 qg.gemm_w4a8_grouped([aq] * G, [copies[j] for j in range(G)], [N] * G, M, K, wt,
@@ -121,7 +145,7 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
         us = graph_time_us(step, reps, G)
         res.append({"wtype": wname, "M": M, "N": N, "K": K, "form": form,
                     "kernel_algo": int(qg.select_algo(M, N, K, wt)),
-                    "us_per_launch" if form == "single" else "us_per_gemv": round(us, 3),
+                    "us_per_launch" if form in ("single", "prepacked", "padded") else "us_per_gemv": round(us, 3),
                     "gbps": round(nbytes / us / 1e3, 1),
                     "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
                     "nmse_vs_fp32": nmse})
@@ -696,7 +720,9 @@ def main() -> None:
             torch.cuda.empty_cache()
             sides = [("q4_0", 32, 4096, 4096, ("single",)), ("q4_1", 1, 4096, 4096, ("single",)),
                      ("q5_0", 1, 4096, 4096, ("single",)), ("q5_1", 1, 4096, 4096, ("single",)),
-                     ("q4_0", 1, 32000, 4096, ("single", "batched"))]
+                     ("q4_0", 1, 32000, 4096, ("single", "batched")),
+                     # odd K/32 at a prefill size from the load-time padded layout
+                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded"))]
             out["side_configs"] = [r for (w, m_, n_, k_, f) in sides for r in measure_config(w, m_, n_, k_, dev, forms=f)]
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -110,6 +110,13 @@ int qg_gemm_w4a8_ws(const void* A_q8_1, const void* B, float* C, int M, int N, i
 size_t qg_repack_weights_bytes(int N, int K, int wtype);
 int qg_repack_weights(const void* B, void* B_packed, int N, int K, int wtype, qg_stream_t stream);
 size_t qg_gemm_w4a8_prepacked_workspace_size(int M, int K);
+/* The activation side of the same layout, written by the quantizer itself so the product is ONE
+ * launch: qg_quantize_q8_1_padded quantizes M rows of K floats (as qg_quantize_q8_1) into rows of
+ * K'/32 Q8_1 blocks, zero blocks after the real ones; qg_gemm_w4a8_padded(A_padded, B_packed, ...)
+ * then runs the QG_ALGO_AUTO kernel on K' directly (K is the logical K). */
+int qg_quantize_q8_1_padded(const float* x, void* y, int M, int K, qg_stream_t stream);
+int qg_gemm_w4a8_padded(const void* A_padded, const void* B_packed, float* C, int M, int N, int K, int wtype,
+                        qg_stream_t stream);
 int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, int M, int N, int K, int wtype,
                            void* workspace, size_t workspace_bytes, qg_stream_t stream);
 

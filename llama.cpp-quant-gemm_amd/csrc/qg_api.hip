@@ -424,6 +424,24 @@ int qg_repack_weights(const void* B, void* B_packed, int N, int K, int wtype, qg
     return hip_status(launch_pad_rows(B, B_packed, N, (K / 32) * bb, padded_blocks(K) * bb, (hipStream_t)stream));
 }
 
+int qg_quantize_q8_1_padded(const float* x, void* y, int M, int K, qg_stream_t stream) {
+    if (M < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (M == 0) return QG_OK;
+    if (!x || !y) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)x & 3) != 0 || ((uintptr_t)y & 3) != 0) return QG_ERR_ALIGN;
+    return hip_status(launch_quantize_q8_1_padded(x, y, M, K / 32, padded_blocks(K), (hipStream_t)stream));
+}
+
+int qg_gemm_w4a8_padded(const void* A_padded, const void* B_packed, float* C, int M, int N, int K, int wtype,
+                        qg_stream_t stream) {
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    GemmArgs g;
+    g.A = A_padded; g.B = B_packed; g.C = C; g.M = M; g.N = N; g.K = padded_blocks(K) * 32; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    return run_gemm(g, QG_ALGO_AUTO, (hipStream_t)stream);
+}
+
 size_t qg_gemm_w4a8_prepacked_workspace_size(int M, int K) {
     if (M <= 0 || K <= 0 || K % 32 != 0 || padded_blocks(K) == K / 32) return 0;
     return (size_t)M * (size_t)padded_blocks(K) * 36;
@@ -463,7 +481,7 @@ int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int
         return g;
     };
     // validate every item before anything is enqueued; one launch only if AUTO picks the GEMV for all
-    bool one_launch = M > 0;
+    bool one_launch = M > 0 && M <= 4;  // the grouped GEMV is instantiated for MT <= 4 (qg_gemv_kernel.hpp)
     for (int i = 0; i < count; ++i) {
         const qg_gemv_item& it = items[i];
         if (it.N < 0 || it.ldc < 0 || (it.ldc != 0 && it.ldc < it.N)) return QG_ERR_INVALID_ARG;

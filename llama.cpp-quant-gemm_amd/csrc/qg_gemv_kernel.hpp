@@ -490,6 +490,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const bool one = g.K / QK / BPL <= LPR;
     // M = 1, one product, unit output stride: the minimal-argument entry (gemv1_kernel)
     const bool m1 = MT == 1 && PRE && !NT && g.M == 1 && g.batch == 1 && g.ldc_n == 1;
+    if (g.group && (SUMI || AIN != AIN_Q8_1 || NT || MT > 4)) return hipErrorInvalidValue;  // no grouped form here
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
         describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
                         LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (int)one,
@@ -497,7 +498,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                         g.batch);
         return hipSuccess;
     }
-    if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT) {
+    if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
         if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
             const GemvGroup& grp = *static_cast<const GemvGroup*>(g.group);
             int tiles = 0;

@@ -89,7 +89,7 @@ bool repack_eligible(const GemmArgs& g);
 // returns hipErrorNotReady (nothing enqueued) when no workspace can be had right now (e.g. capture
 // without a caller workspace g.ws of >= repack_workspace_bytes(g))
 hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st);
-size_t repack_workspace_bytes(const GemmArgs& g);  // weights + activations (+ the sumi image)
+size_t repack_workspace_bytes(const GemmArgs& g);  // padded weights + activations
 // Weights [N][K/32] -> rows of K'/32 = round_up(K/32, 8) blocks, zero blocks after the real ones
 // (qg_repack_weights); activations the same (qg_gemm_w4a8_prepacked). Both enqueue one kernel.
 int padded_blocks(int K);
@@ -116,6 +116,8 @@ void* stream_workspace(hipStream_t st, size_t bytes, int slot = 0, std::unique_l
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st);
 // FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143).
 hipError_t launch_quantize_f16_fused(const void* x, void* y, int64_t nblocks, hipStream_t st);
+// FP32 rows of nb blocks -> Q8_1 rows of nbp blocks, zero blocks after the real ones.
+hipError_t launch_quantize_q8_1_padded(const float* x, void* y, int64_t rows, int nb, int nbp, hipStream_t st);
 hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st);
 
 }  // namespace qg

@@ -207,6 +207,38 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const uint8_t* __restri
     }
 }
 
+// Q8_1 rows of K floats -> rows of nbp >= nb = K/32 blocks: the first nb exactly as quantize_kernel
+// (include/quantize.h:165-193), then zero blocks (d = 0, s = 0) — the activation side of the padded
+// layout of qg_repack_weights (qg_quantize_q8_1_padded, qg_gemm_w4a8_padded).
+template <bool VEC>
+__global__ __launch_bounds__(256) void quantize_q8_1_padded_kernel(const float* __restrict__ x, uint8_t* __restrict__ y,
+                                                                   int64_t rows, int nb, int nbp) {
+    const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ib >= rows * nbp) return;
+    const int64_t r = ib / nbp;
+    const int b = (int)(ib - r * nbp);
+    uint32_t w[9] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (b < nb) {
+        float v[32];
+        load32<VEC>(x + (r * nb + b) * QK, v);
+        quantize_q8_1_block<0>(v, w);
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dst[i] = w[i];
+}
+
+hipError_t launch_quantize_q8_1_padded(const float* x, void* y, int64_t rows, int nb, int nbp, hipStream_t st) {
+    const int64_t n = rows * nbp;
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (((uintptr_t)x & 15) == 0)
+        hipLaunchKernelGGL((quantize_q8_1_padded_kernel<true>), grid, dim3(256), 0, st, x, (uint8_t*)y, rows, nb, nbp);
+    else
+        hipLaunchKernelGGL((quantize_q8_1_padded_kernel<false>), grid, dim3(256), 0, st, x, (uint8_t*)y, rows, nb, nbp);
+    return hipGetLastError();
+}
+
 namespace {
 template <int TYPE, int VARIANT>
 hipError_t lq(const float* x, void* y, int64_t nblocks, hipStream_t st) {

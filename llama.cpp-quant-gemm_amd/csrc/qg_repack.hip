@@ -98,8 +98,7 @@ int padded_blocks(int K) { return (K / QK + PADB - 1) / PADB * PADB; }
 size_t repack_workspace_bytes(const GemmArgs& g) {
     const int nbp = padded_blocks(g.K);
     const long wimg = round256((long)g.N * nbp * wbytes(g.wtype)), aimg = round256((long)g.M * nbp * Q8_1_BYTES);
-    const long simg = g.sumi ? round256((long)g.M * g.N * nbp * 4) : 0;
-    return (size_t)(wimg + aimg + simg);
+    return (size_t)(wimg + aimg);
 }
 
 hipError_t launch_pad_rows(const void* src, void* dst, long rows, int rb, int rbp, hipStream_t st) {
@@ -144,13 +143,22 @@ hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st) {
     g2.A = ws + wimg;
     g2.ws = nullptr;
     g2.ws_bytes = 0;
-    if (g.sumi) g2.sumi = reinterpret_cast<int32_t*>(ws + wimg + aimg);
+    if (!g.sumi) return launch_mfma(g2, st);
+    // parity hook only: the padded sumi image is a stream-ordered temporary (not kept in
+    // the per-stream buffer), compacted to [M][N][K/32] and freed on the stream
+    void* simg = nullptr;
+    e = hipMallocAsync(&simg, (size_t)g.M * g.N * nbp * 4, st);
+    if (e != hipSuccess) return e;
+    g2.sumi = static_cast<int32_t*>(simg);
     e = launch_mfma(g2, st);
-    if (e != hipSuccess || !g.sumi) return e;
-    const long total = (long)g.M * g.N * nb;
-    hipLaunchKernelGGL(sumi_compact_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                       g2.sumi, g.sumi, total, nb, nbp);
-    return hipGetLastError();
+    if (e == hipSuccess) {
+        const long total = (long)g.M * g.N * nb;
+        hipLaunchKernelGGL(sumi_compact_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                           g2.sumi, g.sumi, total, nb, nbp);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(simg, st);
+    return e != hipSuccess ? e : f;
 }
 
 }  // namespace qg

@@ -237,6 +237,36 @@ def gemm_w4a8_prepacked(activation_q: torch.Tensor, weight_packed: torch.Tensor,
     return out
 
 
+def quantize_q8_1_padded(x: torch.Tensor) -> torch.Tensor:
+    """x float32 [M, K] -> uint8 [M, K'/32, 36] (qg_quantize_q8_1_padded): each row's blocks as
+    quantize_q8_1, then zero blocks up to K'/32 = round_up(K/32, 8) — the activation side of the
+    repack_weights layout."""
+    _require(x.is_cuda and x.dtype == torch.float32 and x.dim() == 2, "x must be a 2-D CUDA float32 tensor")
+    M, K = x.shape
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    nbp = (K // 32 + 7) // 8 * 8
+    x = x.contiguous()
+    out = torch.empty((M, nbp, 36), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.load().qg_quantize_q8_1_padded(_ptr(x), _ptr(out), M, K, _stream(x.device)), "quantize_q8_1_padded")
+    return out
+
+
+def gemm_w4a8_padded(activation_padded: torch.Tensor, weight_packed: torch.Tensor, M: int, N: int, K: int,
+                     wtype: int = Q4_0) -> torch.Tensor:
+    """C [M, N] from quantize_q8_1_padded activations and repack_weights weights, one launch
+    (qg_gemm_w4a8_padded; K is the logical K)."""
+    _require(activation_padded.is_cuda and weight_packed.is_cuda, "Inputs must be CUDA tensors")
+    nbp = (K // 32 + 7) // 8 * 8
+    _require(activation_padded.numel() == M * nbp * 36, "Activation shape mismatch")
+    _require(weight_packed.numel() == N * nbp * BLOCK_BYTES[wtype], "Packed weight shape mismatch")
+    out = torch.empty((M, N), dtype=torch.float32, device=weight_packed.device)
+    with torch.cuda.device(weight_packed.device):
+        _lib.check(_lib.load().qg_gemm_w4a8_padded(_ptr(activation_padded.contiguous()), _ptr(weight_packed), _ptr(out),
+                                                   M, N, K, wtype, _stream(weight_packed.device)), "gemm_w4a8_padded")
+    return out
+
+
 def _gemm_weight_major(sym: str, wtype: int, weight_q, activation_q, M, N, K):
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
     _check_blocks(weight_q, "Weight", M, K, BLOCK_BYTES[wtype])

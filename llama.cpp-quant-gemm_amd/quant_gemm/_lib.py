@@ -36,6 +36,8 @@ SIGNATURES = {
     "qg_repack_weights": ([P, P, I, I, I, P], I),
     "qg_gemm_w4a8_prepacked_workspace_size": ([I, I], SZ),
     "qg_gemm_w4a8_prepacked": ([P, P, P, I, I, I, I, P, SZ, P], I),
+    "qg_quantize_q8_1_padded": ([P, P, I, I, P], I),
+    "qg_gemm_w4a8_padded": ([P, P, P, I, I, I, I, P], I),
     "qg_gemm_q4_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q5_0_q8_1": ([P, P, P, I, I, I, P], I),

@@ -52,7 +52,28 @@ static int run(int M, int N, int K) {
     qg::check(qg::quantize_q4_0_cuda(db, dB, (int64_t)b.size(), s), "quantize_q4_0");
     qg::check(qg::gemm_w4a8_naive(dA, dB, dc, M, N, K, s), "gemm_w4a8_naive");          // activation-major
     qg::check(qg::gemm_q4_0_q8_1(dB, dA, dc2, N, M, K, s), "gemm_q4_0_q8_1");          // weight-major [N][M]
+    // the Solution entry point (definition order, integration/solutions/gemm_q4_0_q8_1_hip_gfx950.json)
+    // and the grouped entry (two row halves as two items)
+    float *dc_sol, *dc3;
+    HCK(hipMalloc(&dc_sol, c.size() * 4));
+    HCK(hipMalloc(&dc3, c.size() * 4));
+    if (qg_gemm_q4_0_q8_1_w4a8(dA, dB, dc_sol, M, N, K, s) != QG_OK) return 1;
+    const int half = N / 2;
+    // weight rows [0, half) and [half, N) as two items writing column ranges of one C (ldc = N)
+    qg_gemv_item items[2] = {{dA, dB, dc3, half, N}, {dA, dB + (size_t)half * nb, dc3 + half, N - half, N}};
+    if (M <= 4 && qg_gemm_w4a8_grouped(items, 2, M, K, QG_TYPE_Q4_0, s) != QG_OK) return 1;
     HCK(hipStreamSynchronize(st));
+    {
+        std::vector<float> cs(c.size()), cg(c.size()), c0(c.size());
+        HCK(hipMemcpy(c0.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));
+        HCK(hipMemcpy(cs.data(), dc_sol, c.size() * 4, hipMemcpyDeviceToHost));
+        if (memcmp(cs.data(), c0.data(), c.size() * 4)) { fprintf(stderr, "solution entry differs\n"); return 1; }
+        if (M <= 4) {
+            HCK(hipMemcpy(cg.data(), dc3, c.size() * 4, hipMemcpyDeviceToHost));
+            if (memcmp(cg.data(), c0.data(), c.size() * 4)) { fprintf(stderr, "grouped entry differs\n"); return 1; }
+        }
+    }
+    (void)hipFree(dc_sol); (void)hipFree(dc3);
     HCK(hipMemcpy(aq_gpu.data(), dA, aq.size() * sizeof(qg_block_q8_1), hipMemcpyDeviceToHost));
     HCK(hipMemcpy(bq_gpu.data(), dB, bq.size() * sizeof(qg_block_q4_0), hipMemcpyDeviceToHost));
     HCK(hipMemcpy(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));

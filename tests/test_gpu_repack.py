@@ -107,3 +107,22 @@ def test_repack_strided_and_weight_major(O, qg, t):
     sym = {2: "gemm_q4_0_q8_1", 3: "gemm_q4_1_q8_1", 6: "gemm_q5_0_q8_1", 7: "gemm_q5_1_q8_1", 8: "gemm_q8_0_q8_1"}[t]
     wm = host(getattr(qg, sym)(dev(bq), dev(aq), n, m, k))  # out [N weight rows][M tokens]
     assert np.array_equal(wm.T.view(np.uint32), w[:, :n].view(np.uint32))
+
+
+@pytest.mark.parametrize("t", [2, 3, 8])
+@pytest.mark.parametrize("m,n,k", [(32, 4096, 4128), (3, 300, 1056), (40, 1030, 96)])
+def test_padded_quantizer_and_single_launch(O, qg, t, m, n, k):
+    """qg_quantize_q8_1_padded: the real blocks are qg_quantize_q8_1's bytes (= the oracle's), then
+    zero blocks; qg_gemm_w4a8_padded on them is bit-identical to qg_gemm_w4a8_prepacked (same padded
+    bytes, same kernel) and within the oracle's bound."""
+    a, b = O.fill_uniform_step4(m, n, k, seed=m + k + t)
+    aq, bq = O.quantize(a, O.Q8_1), O.quantize(b, t)
+    ap = host(qg.quantize_q8_1_padded(dev(a)))
+    nb, nbp = k // 32, (k // 32 + 7) // 8 * 8
+    assert ap.shape == (m, nbp, 36)
+    assert np.array_equal(ap[:, :nb], aq) and not ap[:, nb:].any()
+    bp = qg.repack_weights(dev(bq), n, k, t)
+    c = host(qg.gemm_w4a8_padded(dev(ap), bp, m, n, k, t))
+    c2 = host(qg.gemm_w4a8_prepacked(dev(aq), bp, m, n, k, t))
+    assert np.array_equal(c.view(np.uint32), c2.view(np.uint32))
+    close_to_oracle(O, c, aq, bq, t, mfma=qg.select_algo(m, n, 32 * nbp, t) == 2)
