@@ -69,3 +69,49 @@ def test_row_sharded_gather_gloo(world, m, n, k):
         # oracle's own order -> bit-identical to the single-process result
         assert c.shape == (m, n)
         assert np.array_equal(c, ref)
+
+
+def _group_worker(rank, world, port, m, n, k, q):
+    """Several sharded products (G independent weight matrices sharing the activations) computed
+    with RowShardedW4A8.compute_local_group (an injected compute: the products run in turn) and
+    gathered with ONE all-gather of the [G, M, rows] slices, as bench.py's N > 1 legs do."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        from quant_gemm.sharded import RowShardedW4A8, shard_rows
+        G = 3
+        a, _ = O.fill_uniform_step4(m, 0, k, 5)
+        aq = O.quantize(a, O.Q8_1)
+        bqs = [O.quantize(O.fill_uniform_step4(0, n, k, 10 + g)[1], O.Q4_0) for g in range(G)]
+        s0, s1 = shard_rows(n, world, rank)
+
+        def compute(act_q, w_q, M, rows, K, out):
+            out.copy_(torch.from_numpy(O.gemm_w4a8(act_q.numpy(), w_q.numpy(), O.Q4_0)))
+
+        mods = [RowShardedW4A8(torch.from_numpy(b[s0:s1].copy()), n, k, 2, compute=compute) for b in bqs]
+        outs = torch.zeros((G, m, mods[0].rows), dtype=torch.float32)
+        RowShardedW4A8.compute_local_group(mods, torch.from_numpy(aq), m, outs)
+        gathered = torch.empty((world, G, m, mods[0].rows), dtype=torch.float32)
+        mods[0].gather(outs, gathered)
+        res = [RowShardedW4A8.assemble(gathered[:, g], n).numpy().copy() for g in range(G)]
+        q.put((rank, res, [O.gemm_w4a8(aq, b, O.Q4_0) for b in bqs]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,m,n,k", [(2, 1, 64, 256), (3, 2, 50, 256)])
+def test_row_sharded_group_gather_gloo(world, m, n, k):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, m, n, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, cs, refs in res:
+        for c, ref in zip(cs, refs):
+            assert c.shape == (m, n) and np.array_equal(c, ref)
