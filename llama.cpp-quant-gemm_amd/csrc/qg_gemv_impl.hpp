@@ -1,0 +1,70 @@
+// qg_gemv_impl.hpp — the GEMV dispatch templates (configuration per shape), instantiated once per
+// weight format in qg_gemv_<fmt>.hip so the formats compile in parallel; qg_gemv.hip holds the
+// format switch (gemv_eligible, launch_gemv).
+#pragma once
+#include "qg_gemv_kernel.hpp"
+
+// Workgroup size of the M = 1 loop-free GEMV (tuning knob for A/B builds; 1024 = product).
+#ifndef QG_GEMV1_WGS
+#define QG_GEMV1_WGS 1024
+#endif
+
+namespace qg {
+
+template <int F, int MT, bool SUMI, int AIN>
+hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
+    const int nb = g.K / QK;
+    // 2-block units, one row per wave, 1024-thread workgroups (512 for a single row of activations
+    // over N >= 16384 rows): profiles/r01_tuning/gemv_probe_focus.txt, gemv_probe_focus2.txt —
+    // M=1 Q4_0 3.67 -> 3.60 us, Q5_0 / Q5_1 -6 %, M=2 -4 %, M=4 -11 % against 4-block units x 32
+    // lanes x 512 threads; gemv_probe_v2b.txt: N=32000 -3.4 %, K=14336 -3.8 %
+    // (a strided batch uses the same shape, so its outputs equal the single launches' bit for bit;
+    // the fused-quantization prologue is repeated per workgroup, so it keeps 16 rows per workgroup,
+    // with the same per-row summation order)
+    if constexpr (MT <= 4) {
+        if (nb % 2 == 0 && nb / 2 >= 64) {
+            if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
+                return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
+            // activation records preloaded into registers for M <= 4 (tools/gemv_pre_probe.hip,
+            // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
+            if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, QG_GEMV1_WGS, SUMI, AIN, false, true>(g, st);
+            return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN, false, true>(g, st);
+        }
+    }
+    if (nb % 4 == 0) {
+        if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);
+        return gemv_launch<F, MT, 4, 4, 256, SUMI, AIN>(g, st);
+    }
+    return gemv_launch<F, MT, 2, 8, 256, SUMI, AIN>(g, st);
+}
+
+// The sumi parity hook (SUMI = true) runs the very instantiation the product dispatch picks for
+// this shape — same MT, unit size, lanes per row, workgroup size, PRE and loop-free form — and only
+// replaces the final accumulate by a store of each block's int32 dot.
+template <int F, bool SUMI, int AIN> hipError_t launch_m(const GemmArgs& g, hipStream_t st) {
+    if (g.M <= 1) return launch_staged<F, 1, SUMI, AIN>(g, st);
+    if (g.M <= 2) return launch_staged<F, 2, SUMI, AIN>(g, st);
+    if (g.M <= 4) return launch_staged<F, 4, SUMI, AIN>(g, st);
+    return launch_staged<F, 8, SUMI, AIN>(g, st);
+}
+
+template <int F> hipError_t launch_f(const GemmArgs& g, hipStream_t st) {
+    if (g.sumi) return launch_m<F, true, AIN_Q8_1>(g, st);
+    if (g.ain == AIN_F32) return launch_m<F, false, AIN_F32>(g, st);
+    if (g.ain == AIN_F16_FUSED) return launch_m<F, false, AIN_F16_FUSED>(g, st);
+    return launch_m<F, false, AIN_Q8_1>(g, st);
+}
+
+template <int F> bool ok_f(const GemmArgs& g) {
+    return (g.K / QK) % 4 == 0 ? gemv_shape_ok<F, 4>(g) : gemv_shape_ok<F, 2>(g);
+}
+
+// one explicit specialization per format (qg_gemv_<fmt>.hip)
+template <int F> hipError_t gemv_launch_fmt(const GemmArgs& g, hipStream_t st);
+template <> hipError_t gemv_launch_fmt<FMT_Q4_0>(const GemmArgs& g, hipStream_t st);
+template <> hipError_t gemv_launch_fmt<FMT_Q4_1>(const GemmArgs& g, hipStream_t st);
+template <> hipError_t gemv_launch_fmt<FMT_Q5_0>(const GemmArgs& g, hipStream_t st);
+template <> hipError_t gemv_launch_fmt<FMT_Q5_1>(const GemmArgs& g, hipStream_t st);
+template <> hipError_t gemv_launch_fmt<FMT_Q8_0>(const GemmArgs& g, hipStream_t st);
+
+}  // namespace qg

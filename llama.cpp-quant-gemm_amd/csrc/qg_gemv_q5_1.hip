@@ -1,0 +1,7 @@
+// qg_gemv_q5_1.hip — the GEMV kernels for Q5_1 weights (qg_gemv_impl.hpp); one translation unit per
+// weight format so the product library's largest template set compiles in parallel.
+#include "qg_gemv_impl.hpp"
+
+namespace qg {
+template <> hipError_t gemv_launch_fmt<FMT_Q5_1>(const GemmArgs& g, hipStream_t st) { return launch_f<FMT_Q5_1>(g, st); }
+}  // namespace qg
