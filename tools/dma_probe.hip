@@ -92,6 +92,60 @@ __global__ __launch_bounds__((LW + EXTRA) * 64) void dma_kernel(const uint8_t* _
     if (lane == 0 && K < 0) sink[blockIdx.x] = (float)smem[wave];
 }
 
+// Split roles: WL waves stream only the weight pieces of the stages (stage h by weight loader h % WL),
+// AL waves only the activation pieces (stage h by activation loader h % AL); ORDER 0: both start at
+// once; 1: activation loaders first issue ALL their stages (L2-resident lines, 73.7 KB), weights
+// stream meanwhile with depth DW.
+constexpr int WNI = (WPC + 63) / 64;  // 3 weight instructions per stage (160 pieces)
+constexpr int ANI = (APC + 63) / 64;  // 3 activation instructions per stage (144 pieces)
+template <int WL, int AL, int DW, int DA>
+__global__ __launch_bounds__((WL + AL) * 64) void dma_split_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                                   int K, float* __restrict__ sink) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nb = K / QK, H = nb / SB;
+    const long RB = (long)nb * 18, AB = (long)nb * 36;
+    const uint8_t* Bw = B + (long)blockIdx.x * BN * RB;
+    const uint8_t* Aw = A + (long)blockIdx.y * NTOK * AB;
+    const bool wl = wave < WL;
+    const int me = wl ? wave : wave - WL, L = wl ? WL : AL;
+    const int NIW = wl ? WNI : ANI;
+    int coff[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (wl) {
+            const int p = min(64 * i + lane, WPC - 1);
+            coff[i] = (p / PPR) * (int)RB + (p % PPR) * 16;
+        } else {
+            const int p = min(64 * i + lane, APC - 1);
+            coff[i] = (p / APT) * (int)AB + (p % APT) * 16;
+        }
+    }
+    auto issue = [&](int h) {
+        const uint8_t* src = wl ? Bw + (long)h * RSB - ((h * RSB) & 15) : Aw + (long)h * (SB * 36);
+        uint8_t* buf = smem + (h % 26) * 6144 + (wl ? 0 : 3072);  // 26 x 6 KB < 160 KB (probe: slot reuse unguarded)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) glds16(src + coff[i], buf + 64 * i * 16);
+    };
+    const int D = wl ? DW : DA;
+    const int mine = (H - 1 - me) / L + 1;
+    int issued = 0;
+    for (; issued < D && issued < mine; ++issued) issue(me + issued * L);
+    for (int k = 0; k < mine; ++k) {
+        const int younger = min(issued - k - 1, D - 1);
+        if (younger >= 8) vm_wait<24>();
+        else if (younger >= 4) vm_wait<12>();
+        else if (younger >= 2) vm_wait<6>();
+        else if (younger == 1) vm_wait<3>();
+        else vm_wait<0>();
+        if (issued < mine) issue(me + (issued++) * L);
+    }
+    vm_wait<0>();
+    (void)NIW;
+    if (lane == 0 && K < 0) sink[blockIdx.x] = (float)smem[wave];
+}
+
 typedef std::function<void(const uint8_t*, const uint8_t*, hipStream_t)> Fn;
 
 template <int LW, int DEPTH, int NS, int MODE, int EXTRA = 0>
@@ -102,6 +156,18 @@ Fn mk(int K, float* sink) {
         static bool set = false;
         if (!set) { CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); set = true; }
         hipLaunchKernelGGL(k, dim3(128, 2), dim3((LW + EXTRA) * 64), lds, st, A, B, K, sink);
+    };
+}
+
+template <int WL, int AL, int DW, int DA>
+Fn mks(int K, float* sink) {
+    return [=](const uint8_t* A, const uint8_t* B, hipStream_t st) {
+        auto k = dma_split_kernel<WL, AL, DW, DA>;
+        const size_t lds = 32 * 6144;  // 192 KB? no: 32 stages x 6 KB = 192 KB > LDS -> stages reuse mod 26
+        static bool set = false;
+        if (!set) { CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); set = true; }
+        (void)lds;
+        hipLaunchKernelGGL(k, dim3(128, 2), dim3((WL + AL) * 64), 160 * 1024, st, A, B, K, sink);
     };
 }
 
@@ -134,6 +200,12 @@ int main() {
         {"lw4 d4 ns32 acts", mk<4, 4, 32, 2>(K, sink)},
         {"lw8 d2 ns32 weights", mk<8, 2, 32, 1>(K, sink)},
         {"lw8 d2 ns32 acts", mk<8, 2, 32, 2>(K, sink)},
+        {"split w2 a1 dw4 da8", mks<2, 1, 4, 8>(K, sink)},
+        {"split w2 a2 dw4 da8", mks<2, 2, 4, 8>(K, sink)},
+        {"split w4 a1 dw4 da16", mks<4, 1, 4, 16>(K, sink)},
+        {"split w4 a2 dw2 da8", mks<4, 2, 2, 8>(K, sink)},
+        {"split w2 a1 dw8 da16", mks<2, 1, 8, 16>(K, sink)},
+        {"split w4 a4 dw4 da4", mks<4, 4, 4, 4>(K, sink)},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
