@@ -8,6 +8,9 @@
 #include <vector>
 #include "qg_mmq_kernel.hpp"
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+namespace qg {
+void describe_kernel(const GemmArgs&, const char*, ...) {}
+}
 using namespace qg;
 static uint16_t f2h(float f) { _Float16 h = (_Float16)f; uint16_t b; memcpy(&b, &h, 2); return b; }
 template <int BN, int TT, int W, bool P16>
@@ -28,7 +31,8 @@ static void run(const char* name, int M, int N, int K) {
     const int L = 100;
     for (int rep = 0; rep < 2; ++rep) {
         CK(hipEventRecord(e0, 0));
-        for (int i = 0; i < L; ++i) { g.B = w[i % R]; CK((mmq_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, 0))); }
+        // the product's instantiation (qg_gemm_mfma.hip run_p: NB 2, SB 4, EPI2, general entry)
+        for (int i = 0; i < L; ++i) { g.B = w[i % R]; CK((mmq_launch<FMT_Q4_0, BN, TT, W, false, P16, 2, 0, false, 4, 1, true>(g, 0))); }
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         const int nwg = ((N + BN - 1) / BN) * ((M + 16 * TT - 1) / (16 * TT)), nw = nwg * W;
@@ -49,13 +53,16 @@ static void run(const char* name, int M, int N, int K) {
         printf("%s M=%d N=%d K=%d rep%d: event %.2f us/launch, span %.2f us, %d waves\n", name, M, N, K, rep, ms * 1e3 / L, (tend - t0) * 0.01, nw);
         const char* names[5] = {"entry offset", "entry->first data", "first sb compute", "entry->main loop done", "reduction+store"};
         for (int k = 0; k < 5; ++k) printf("   %-22s p10 %5.2f p50 %5.2f p90 %5.2f max %5.2f\n", names[k], pct(seg[k], .1), pct(seg[k], .5), pct(seg[k], .9), pct(seg[k], 1.0));
+        // per-CU ingest: one workgroup per CU; its L2 -> LDS bytes (weights BN rows x K, activations
+        // 16 TT tokens x K as Q8_1) over its waves' entry -> main-loop-done span
+        const double wg_bytes = (double)BN * nb * 18 + 16.0 * TT * nb * 36;
+        printf("   per-workgroup L2->LDS bytes %.0f; ingest at the p50 / p90 main-loop span: %.1f / %.1f GB/s per CU\n",
+               wg_bytes, wg_bytes / (pct(seg[3], .5) * 1e3), wg_bytes / (pct(seg[3], .9) * 1e3));
     }
     for (auto p : w) CK(hipFree(p));
     CK(hipFree(a)); CK(hipFree(c));
 }
 int main() {
-    run<32, 1, 8, false>("bn32 tt1 w8 p4", 32, 4096, 4096);
-    run<32, 1, 8, true>("bn32 tt1 w8 p16", 32, 4096, 4096);
-    run<32, 4, 4, true>("bn32 tt4 w4 p16", 512, 4096, 4096);
+    run<32, 1, 8, true>("product bn32 tt1 w8 p16 epi2", 32, 4096, 4096);
     return 0;
 }
