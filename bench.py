@@ -238,6 +238,25 @@ def _timed_runs(fn, seconds: float):
     return times[n // 2], times[n // 10], times[(9 * n) // 10], n, time.perf_counter() - t0
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup grants this process (cgroup v2 cpu.max 'quota period', v1 cfs files), rounded
+    up; None when unlimited or unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else max(1, -(-q // per))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
     """the reference is single-threaded -> the headline baseline is 1 core, pinned
     (sched_setaffinity, as taskset), after 1 warm-up, median of the runs; beside it the product's
@@ -268,15 +287,18 @@ def cpu_baseline(m: int, n: int, k: int, wtype: int, seconds: float):
                 "sample": f"the product's host twin libqg_host.so qg_gemm_w4a8_cpu_mt (restates "
                           f"include/gemm_reference.h:175-222), 1 thread pinned to core {core}, median of {twin[3]} runs"}
     # row-partitioned runs over the twin's persistent pool: 16 threads (the box's CPU share for one
-    # GPU) and nproc (every core this process may use)
+    # GPU) and every core this process may run on — the affinity set, capped by the
+    # cgroup CPU quota (nproc counts the host's cores, the quota is what the process gets)
     nproc = len(saved) if saved else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    usable = min(nproc, quota) if quota else nproc
     mts = []
-    for threads in sorted({min(16, nproc), nproc}):
+    for threads in sorted({min(16, usable), usable}):
         mt = _timed_runs(lambda: qhost.gemm_w4a8(aq, bq, m, n, k, wtype, threads), max(1.0, seconds / 5))
         mts.append({"value": flops / mt[0] / 1e12, "unit": "TFLOPS", "cores": threads, "ms_per_gemv": mt[0] * 1e3,
                     "ms_p10_p90": ms3(mt[1:3]), "cpu": model,
                     "sample": f"libqg_host.so row-partitioned over a persistent pool of {threads} threads "
-                              f"(nproc {nproc}), median of {mt[3]} runs"})
+                              f"(nproc {nproc}, cgroup CPU quota {quota or 'none'}), median of {mt[3]} runs"})
     return ({"value": flops / per / 1e12, "unit": "TFLOPS", "cores": 1, "kind": "port",
              "ms_per_gemv": per * 1e3, "ms_p10_p90": ms3((p10, p90)), "cpu": model,
              "sample": f"oracle/qg_oracle.c gemm_w4a8 (restates include/gemm_reference.h:175-222), "
