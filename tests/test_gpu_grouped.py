@@ -79,6 +79,24 @@ def test_grouped_more_than_64_items(O, qg):
         assert np.array_equal(host(outs[i]).view(np.uint32), single.view(np.uint32)), f"item {i}"
 
 
+@pytest.mark.parametrize("m", [1, 2])
+def test_grouped_mixed_config_rows(O, qg, m):
+    """A group whose largest item picks another GEMV workgroup shape (M = 1, N >= 16384: 512-thread
+    workgroups, qg_gemv_impl.hpp) than its small items alone: the per-row summation order is the
+    same, so every item stays bit-identical to its own single launch."""
+    rng = np.random.default_rng(40 + m)
+    t, k = 2, 4096
+    ns = [32000, 4096, 1000]
+    aqs, bqs = _case(O, rng, m, ns, k, t)
+    a_d = dev(aqs[0])
+    b_d = [dev(b) for b in bqs]
+    outs = qg.gemm_w4a8_grouped([a_d] * 3, b_d, ns, m, k, t)
+    for i, n in enumerate(ns):
+        single = host(qg.gemm_w4a8(a_d, b_d[i], m, n, k, t))
+        assert np.array_equal(host(outs[i]).view(np.uint32), single.view(np.uint32)), f"item {i}"
+    close_to_oracle(O, host(outs[2]), aqs[2], bqs[2], t)
+
+
 @pytest.mark.parametrize("m,k", [(8, 4096), (1, 4128), (3, 4128), (32, 1024)])
 def test_grouped_per_item_path(O, qg, m, k):
     """Shapes AUTO does not send to the GEMV (M > 4, odd K/32): items enqueued one by one, same bits."""
