@@ -135,7 +135,8 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
  * call outside stream capture. Calls made during stream capture never use the library's
  * workspace: they run without split-K (same results to fp32 summation order), so a graph holds
- * no pointer the library may free. qg_release_workspaces() frees them (after a device synchronize).
+ * no pointer the library may free. qg_release_workspaces() frees them (after a device synchronize;
+ * call it when no other thread is inside the library, e.g. at teardown).
  * The _ws forms take the caller's workspace instead (for graphs and multi-stream callers):
  * >= qg_gemm_w16_workspace_size(M, N, K) bytes (0: no split-K for this shape), 256-B aligned,
  * zeroed once before its first use. Its layout is shape-independent: a counter region that every

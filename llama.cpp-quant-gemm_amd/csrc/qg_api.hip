@@ -1,9 +1,12 @@
 // qg_api.hip — the C-ABI (include/qg/qg.h): validation, dispatch, error reporting.
 //
-// No host synchronisation: every entry point validates, picks a kernel family and enqueues on the
-// caller's stream, so callers may capture it into a hipGraph. The one allocation is the split-K
-// workspace of the W4A16 / W8A16 prefill (stream_workspace below): made once per (device, stream)
-// outside capture and never used by a captured call (which runs the kernel without split-K).
+// Every entry point validates, picks a kernel family and enqueues on the caller's stream, so
+// callers may capture it into a hipGraph. The library's only allocations are the per-(device,
+// stream) workspaces of stream_workspace below — slot 0 the W4A16 / W8A16 split-K partials, slot 1
+// the odd-K/32 prefill's padded copies — made outside capture, never handed to a captured call
+// (captured calls take the non-workspace kernels, or the caller's buffer through the _ws entry
+// points), and grown only: growing one synchronizes its stream once (the library's one host sync,
+// qg.h), qg_release_workspaces frees them.
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
