@@ -16,7 +16,6 @@
 #include <vector>
 
 #include "gemv_experiments.hpp"  // + the product header qg_gemv_kernel.hpp
-#include "gemv_v1.hpp"           // the round-1 product kernel (A/B baseline)
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -143,8 +142,6 @@ static void bench(Problem& p, std::vector<Variant>& vs, hipStream_t st, int roun
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, true>(g, s); }, false});
 #define NOPRE(F, MT, BPL, LPR, WGS, NAME) \
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_launch<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, false>(g, s); }, false});
-#define V1(F, MT, BPL, LPR, WGS, NAME) \
-    vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_v1_launch<F, MT, BPL, LPR, WGS, 4 * MT, false>(g, s); }, false});
 #define RAX(F, MT, BPL, LPR, WGS, PF, NAME) \
     vs.push_back({NAME, [](const GemmArgs& g, hipStream_t s) { return gemv_ra_launch<F, MT, BPL, LPR, WGS, PF, false>(g, s); }, false});
 
@@ -159,7 +156,6 @@ static void add_read(std::vector<Variant>& vs, Problem& p) {
 }
 
 template <int F> static void m1(std::vector<Variant>& vs, bool full) {
-    V1(F, 1, 4, 32, 512, "v1 bpl4 lpr32 wg512")
     STAGED(F, 1, 4, 32, 512, "v2 bpl4 lpr32 wg512")
     STAGED(F, 1, 4, 32, 256, "v2 bpl4 lpr32 wg256")
     STAGED(F, 1, 2, 64, 512, "v2 bpl2 lpr64 wg512")
@@ -203,7 +199,6 @@ int main(int argc, char** argv) {
             if (s.F == FMT_Q5_1) m1<FMT_Q5_1>(vs, full);
             add_read(vs, p);
         } else if (s.M == 2) {
-            V1(FMT_Q4_0, 2, 4, 32, 512, "v1 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 2, 4, 32, 512, "v2 pre bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 2, 2, 64, 1024, "v2 pre bpl2 lpr64 wg1024")
             STAGED(FMT_Q4_0, 2, 2, 64, 512, "v2 pre bpl2 lpr64 wg512")
@@ -212,14 +207,12 @@ int main(int argc, char** argv) {
             RAX(FMT_Q4_0, 2, 4, 32, 256, true, "ra bpl4 lpr32 wg256 pf")
             RAX(FMT_Q4_0, 2, 2, 64, 256, false, "ra bpl2 lpr64 wg256")
         } else if (s.M == 4) {
-            V1(FMT_Q4_0, 4, 4, 32, 512, "v1 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 4, 4, 32, 512, "v2 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 4, 2, 64, 1024, "v2 bpl2 lpr64 wg1024")
             STAGED(FMT_Q4_0, 4, 4, 32, 256, "staged bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 4, 32, 256, false, "ra bpl4 lpr32 wg256")
             RAX(FMT_Q4_0, 4, 2, 64, 256, false, "ra bpl2 lpr64 wg256")
         } else {
-            V1(FMT_Q4_0, 8, 4, 32, 512, "v1 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 8, 4, 32, 512, "v2 bpl4 lpr32 wg512")
             STAGED(FMT_Q4_0, 8, 4, 32, 256, "staged bpl4 lpr32 wg256")
             STAGED(FMT_Q4_0, 8, 2, 64, 512, "staged bpl2 lpr64 wg512")

@@ -15,7 +15,6 @@
 #include <vector>
 
 #include "qg_mmq_kernel.hpp"
-#include "mmq_v1.hpp"
 #include "mmq_tile_experiment.hpp"  // measured slower than the product, kept for the record  // round-1 product kernel (A/B baseline)
 #include "../include/qg/qg.h"
 
@@ -64,11 +63,6 @@ int main() {
         // Q4_0 configurations only (other formats: the product dispatch above)
 #define V(BN, TT, W, P16, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, P16>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, st) : hipErrorInvalidValue; }});
-#define V1(BN, TT, W, P16, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
-        return g.wtype == FMT_Q4_0 && mmq_v1_shape_ok<FMT_Q4_0, BN, TT, W, P16>(g) ? mmq_v1_launch<FMT_Q4_0, BN, TT, W, false, P16>(g, st) : hipErrorInvalidValue; }});
-        V1(32, 1, 8, true, "v1 bn32 tt1 w8 p16")
-        V1(16, 1, 8, true, "v1 bn16 tt1 w8 p16")
-        V1(32, 2, 8, true, "v1 bn32 tt2 w8 p16")
 #define VN(BN, TT, W, NB, NAME) vs.push_back({NAME, [](const GemmArgs& g, hipStream_t st) { \
         return g.wtype == FMT_Q4_0 && mmq_shape_ok<FMT_Q4_0, BN, TT, W, true, NB>(g) ? mmq_launch<FMT_Q4_0, BN, TT, W, false, true, NB>(g, st) : hipErrorInvalidValue; }});
         VN(32, 1, 8, 2, "v2 bn32 tt1 w8 nb2")
