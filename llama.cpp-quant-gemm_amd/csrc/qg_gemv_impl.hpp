@@ -27,7 +27,10 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
                 return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
             // activation records preloaded into registers for M <= 4 (tools/gemv_pre_probe.hip,
             // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
-            if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, QG_GEMV1_WGS, SUMI, AIN, false, true>(g, st);
+            // Q5_0 / Q5_1: 512-thread workgroups (profiles/r03_tuning/r03_ab_wgs.txt: M=1 3.82 -> 3.78 /
+            // 3.93 -> 3.88 us; Q4_0 / Q8_0 are faster at 1024, Q4_1 equal)
+            constexpr int W1 = (F == FMT_Q5_0 || F == FMT_Q5_1) ? 512 : QG_GEMV1_WGS;
+            if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, W1, SUMI, AIN, false, true>(g, st);
             return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN, false, true>(g, st);
         }
     }
