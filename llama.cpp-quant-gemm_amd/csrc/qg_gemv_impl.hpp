@@ -8,8 +8,22 @@
 #ifndef QG_GEMV1_WGS
 #define QG_GEMV1_WGS 1024
 #endif
+// tuning knobs (A/B builds): M = 2..4 workgroup size (0: per format, below); M = 1, N >= 16384
+// workgroup size
+#ifndef QG_GEMVM_WGS
+#define QG_GEMVM_WGS 0
+#endif
+#ifndef QG_GEMVBIG_WGS
+#define QG_GEMVBIG_WGS 512
+#endif
 
 namespace qg {
+
+// M = 2..4: 512-thread workgroups for the byte-decode formats (profiles/r03_tuning/r03_ab_m512.txt:
+// Q5_0 M=2 4.41 -> 4.29 us, Q5_1 M=4 5.99 -> 5.75, Q8_0 M=4 5.87 -> 5.62), 1024 for the nibble-plane
+// ones (Q4_1 M=2 3.78 -> 4.01 at 512; Q4_0 M=2 -0.06 but M=4 +0.02)
+template <int F>
+constexpr int gemvm_wgs = QG_GEMVM_WGS ? QG_GEMVM_WGS : (F == FMT_Q5_0 || F == FMT_Q5_1 || F == FMT_Q8_0) ? 512 : 1024;
 
 template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
@@ -24,14 +38,14 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
     if constexpr (MT <= 4) {
         if (nb % 2 == 0 && nb / 2 >= 64) {
             if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
-                return gemv_launch<F, 1, 2, 64, 512, SUMI, AIN>(g, st);
+                return gemv_launch<F, 1, 2, 64, QG_GEMVBIG_WGS, SUMI, AIN>(g, st);
             // activation records preloaded into registers for M <= 4 (tools/gemv_pre_probe.hip,
             // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
             // Q5_0 / Q5_1: 512-thread workgroups (profiles/r03_tuning/r03_ab_wgs.txt: M=1 3.82 -> 3.78 /
             // 3.93 -> 3.88 us; Q4_0 / Q8_0 are faster at 1024, Q4_1 equal)
             constexpr int W1 = (F == FMT_Q5_0 || F == FMT_Q5_1) ? 512 : QG_GEMV1_WGS;
             if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, W1, SUMI, AIN, false, true>(g, st);
-            return gemv_launch<F, MT, 2, 64, 1024, SUMI, AIN, false, true>(g, st);
+            return gemv_launch<F, MT, 2, 64, MT == 1 ? 1024 : gemvm_wgs<F>, SUMI, AIN, false, true>(g, st);
         }
     }
     if (nb % 4 == 0) {
