@@ -13,6 +13,9 @@
 #ifndef QG_GEMVM_WGS
 #define QG_GEMVM_WGS 0
 #endif
+#ifndef QG_GEMV1L_WGS
+#define QG_GEMV1L_WGS 0  // M = 1 with the unit loop (K > 4096); 0: per format, below
+#endif
 #ifndef QG_GEMVBIG_WGS
 #define QG_GEMVBIG_WGS 512
 #endif
@@ -24,6 +27,9 @@ namespace qg {
 // ones (Q4_1 M=2 3.78 -> 4.01 at 512; Q4_0 M=2 -0.06 but M=4 +0.02)
 template <int F>
 constexpr int gemvm_wgs = QG_GEMVM_WGS ? QG_GEMVM_WGS : (F == FMT_Q5_0 || F == FMT_Q5_1 || F == FMT_Q8_0) ? 512 : 1024;
+// M = 1, K > 4096 (the unit loop): 512 for Q8_0 (r03_ab_l512.txt: K=11008 10.60 -> 9.72 us, K=14336
+// 12.64 -> 12.36), 1024 for the rest (Q4_0 / Q4_1 +3 %, Q5_x equal at 512)
+template <int F> constexpr int gemv1l_wgs = QG_GEMV1L_WGS ? QG_GEMV1L_WGS : F == FMT_Q8_0 ? 512 : 1024;
 
 template <int F, int MT, bool SUMI, int AIN>
 hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
@@ -45,7 +51,7 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
             // 3.93 -> 3.88 us; Q4_0 / Q8_0 are faster at 1024, Q4_1 equal)
             constexpr int W1 = (F == FMT_Q5_0 || F == FMT_Q5_1) ? 512 : QG_GEMV1_WGS;
             if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, W1, SUMI, AIN, false, true>(g, st);
-            return gemv_launch<F, MT, 2, 64, MT == 1 ? 1024 : gemvm_wgs<F>, SUMI, AIN, false, true>(g, st);
+            return gemv_launch<F, MT, 2, 64, MT == 1 ? gemv1l_wgs<F> : gemvm_wgs<F>, SUMI, AIN, false, true>(g, st);
         }
     }
     if (nb % 4 == 0) {
