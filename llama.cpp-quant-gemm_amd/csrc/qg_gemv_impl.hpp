@@ -16,6 +16,9 @@
 #ifndef QG_GEMV1L_WGS
 #define QG_GEMV1L_WGS 0  // M = 1 with the unit loop (K > 4096); 0: per format, below
 #endif
+#ifndef QG_GEMV_SMALLK
+#define QG_GEMV_SMALLK 1  // K < 4096 shapes on 16-row workgroups (0: the round-2 64-row form, A/B builds)
+#endif
 #ifndef QG_GEMVBIG_WGS
 #define QG_GEMVBIG_WGS 512
 #endif
@@ -53,6 +56,12 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
             if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, W1, SUMI, AIN, false, true>(g, st);
             return gemv_launch<F, MT, 2, 64, MT == 1 ? gemv1l_wgs<F> : gemvm_wgs<F>, SUMI, AIN, false, true>(g, st);
         }
+    }
+    if constexpr (QG_GEMV_SMALLK && MT <= 4) {
+        // K < 4096: 2-block units, 32 / 16 lanes per row, 16 rows per workgroup (256 workgroups at
+        // N = 4096) instead of 64-row workgroups of 4-lane rows
+        if (nb % 2 == 0 && nb / 2 >= 32) return gemv_launch<F, MT, 2, 32, 512, SUMI, AIN, false, true>(g, st);
+        if (nb % 2 == 0 && nb / 2 >= 16) return gemv_launch<F, MT, 2, 16, 256, SUMI, AIN, false, true>(g, st);
     }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return gemv_launch<F, MT, 4, 32, 512, SUMI, AIN>(g, st);

@@ -39,6 +39,25 @@ template <int F> __device__ __forceinline__ float w16_elem(uint32_t x, int j) {
     else return (float)((x >> (8 * j)) & 0xFFu) - 8.0f;
 }
 
+// One block of a lane's unit against its activation records (registers or LDS): element pairs on
+// the packed-f32 ALU — byte -> f32 (v_cvt_f32_ubyte*), minus the offset as one v_pk_add per pair
+// (Q8_0: sign bit flipped first, offset 128), one v_pk_fma per pair into two pair accumulators;
+// exact weight values.
+template <int F> __device__ __forceinline__ float w16_block_dot(const wblock& wb, const float4* a4) {
+    constexpr float OFF = F == FMT_Q8_0 ? -128.0f : -8.0f;
+    f32x2 p0 = {0.0f, 0.0f}, p1 = {0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t x = F == FMT_Q8_0 ? wb.q[i] ^ 0x80808080u : wb.q[i];
+        const f32x2 w0 = f32x2{(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)} + f32x2{OFF, OFF};
+        const f32x2 w1 = f32x2{(float)((x >> 16) & 0xFFu), (float)(x >> 24)} + f32x2{OFF, OFF};
+        const float4 a = a4[i];
+        p0 = __builtin_elementwise_fma(f32x2{a.x, a.y}, w0, p0);
+        p1 = __builtin_elementwise_fma(f32x2{a.z, a.w}, w1, p1);
+    }
+    return (p0.x + p1.x) + (p0.y + p1.y);
+}
+
 // ONEU (MT == 1, K <= 32 * BPL * LPR): every lane owns at most one unit, so there is no unit loop;
 // the lane's activation records are read into registers right after the staging barrier, before
 // its weights land (as the W4A8 GEMV's PRE / ONEU, qg_gemv_kernel.hpp), leaving only VALU work
@@ -101,24 +120,7 @@ const int row = blockIdx.x * RPB + (tid >> 6) * RPW + lane / LPR;
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
 
-    // one block of this lane's unit against its activation records (registers or LDS)
-    auto block_dot = [&](const wblock& wb, const float4* a4) {
-        // element pairs on the packed-f32 ALU: byte -> f32 (v_cvt_f32_ubyte*), minus the offset as
-        // one v_pk_add per pair (Q8_0: sign bit flipped first, offset 128), one v_pk_fma per pair
-        // into two pair accumulators; exact weight values
-        constexpr float OFF = F == FMT_Q8_0 ? -128.0f : -8.0f;
-        f32x2 p0 = {0.0f, 0.0f}, p1 = {0.0f, 0.0f};
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t x = F == FMT_Q8_0 ? wb.q[i] ^ 0x80808080u : wb.q[i];
-            const f32x2 w0 = f32x2{(float)(x & 0xFFu), (float)((x >> 8) & 0xFFu)} + f32x2{OFF, OFF};
-            const f32x2 w1 = f32x2{(float)((x >> 16) & 0xFFu), (float)(x >> 24)} + f32x2{OFF, OFF};
-            const float4 a = a4[i];
-            p0 = __builtin_elementwise_fma(f32x2{a.x, a.y}, w0, p0);
-            p1 = __builtin_elementwise_fma(f32x2{a.z, a.w}, w1, p1);
-        }
-        return (p0.x + p1.x) + (p0.y + p1.y);
-    };
+    auto block_dot = [&](const wblock& wb, const float4* a4) { return w16_block_dot<F>(wb, a4); };
     if constexpr (ONEU) {
         static_assert(MT == 1, "one activation row");
         const int u = lir;
@@ -182,6 +184,72 @@ template <int F, int BPL, int LPR, int WGS, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void w16_gemv1_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                         int K, float* __restrict__ C) {
     w16_gemv_body<F, 1, BPL, LPR, WGS, ONEU>(A, B, 0, 1, N, K, C, 0, 0, 1);
+}
+
+// M = 1, one 2-block unit per lane (K <= 4096), RPL weight rows per wave: the lane reads its 64
+// activation floats from LDS once and uses them for RPL rows (rows w, w + W, ... of the workgroup's
+// RPL * W), so the workgroup's LDS reads shrink RPL-fold (each row needs all K activations; with one
+// row per wave a CU re-reads the 16 KB vector 16 times). Per row the same summation order as the
+// one-row kernel: bit-identical outputs.
+template <int F, int WGS, int RPL>
+__global__ __launch_bounds__(WGS) void w16_gemv1r_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B, int N,
+                                                         int K, float* __restrict__ C) {
+    using G = w16_geom<F, 2>;
+    constexpr int W = WGS / 64;
+    extern __shared__ __attribute__((aligned(16))) float lds_f[];
+    const int nb = K / QK, U = nb / 2;  // U <= 64
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k4 = K / 4;
+    constexpr int NPRE = 4;
+    float4 av[NPRE];
+#pragma unroll
+    for (int i = 0; i < NPRE; ++i) {
+        const int g = tid + i * WGS;
+        av[i] = g < k4 ? reinterpret_cast<const float4*>(A)[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    uint32_t cur[RPL][G::UDW];
+    const int u = lane < U ? lane : 0;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+        const int row = blockIdx.x * (W * RPL) + j * W + wave;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(B + (long)(row < N ? row : 0) * ((long)U * G::UB) + (long)u * G::UB);
+#pragma unroll
+        for (int v = 0; v < G::UDW; ++v) cur[j][v] = p[v];
+    }
+    auto stage = [&](int g, float4 v) {
+        const int b = g >> 3, uu = b >> 1;
+        *reinterpret_cast<float4*>(lds_f + uu * G::REC_DW + (b & 1) * 32 + (g & 7) * 4) = v;
+    };
+#pragma unroll
+    for (int i = 0; i < NPRE; ++i) {
+        const int g = tid + i * WGS;
+        if (g < k4) stage(g, av[i]);
+    }
+    for (int g = tid + NPRE * WGS; g < k4; g += WGS) stage(g, reinterpret_cast<const float4*>(A)[g]);
+    __syncthreads();
+    float acc[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) acc[j] = 0.0f;
+    if (lane < U) {
+        float4 pre[2][8];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pre[bi][i] = *reinterpret_cast<const float4*>(lds_f + lane * G::REC_DW + bi * 32 + 4 * i);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < RPL; ++j)
+            static_for<2>([&](auto BI) {
+                const wblock wb = decode_block<F, decltype(BI)::value>(cur[j]);
+                acc[j] = __builtin_fmaf(wb.d, w16_block_dot<F>(wb, pre[decltype(BI)::value]), acc[j]);
+            });
+    }
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+        acc[j] = group_sum_last<64>(acc[j]);
+        const int row = blockIdx.x * (W * RPL) + j * W + wave;
+        if (lane == 63 && row < N) C[row] = acc[j];
+    }
 }
 
 // Any K % 32 == 0 and alignment: one wave per output element, lanes stride over blocks.
@@ -1024,6 +1092,12 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
     if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef QG_GEMV_SMALLK
+#define QG_GEMV_SMALLK 1
+#endif
+#ifndef QG_W16_RPL
+#define QG_W16_RPL 1  // weight rows per wave of the M = 1 W4A16 GEMV (tuning knob; 1 = w16_gemv1_kernel)
+#endif
 namespace {
 constexpr int W16_MT = 8;
 constexpr size_t W16_LDS_MAX = 160 * 1024;
@@ -1064,8 +1138,28 @@ template <int F, int MT> hipError_t w16_launch_mt(const GemmArgs& g, hipStream_t
     if (MT <= 4 && nb % 2 == 0 && nb / 2 >= 64 && w16_lds<F, 2>(g.M < MT ? g.M : MT, g.K) <= W16_LDS_MAX) {
         // K == 4096, Q4_0: one unit per lane (M=1 4.82 -> 4.61 us; Q8_0 measured no better)
         if constexpr (MT == 1 && F == FMT_Q4_0)
-            if (nb / 2 <= 64) return w16_launch<F, 1, 2, 64, 1024, true>(g, st);
+            if (nb / 2 <= 64) {
+                if (QG_W16_RPL > 1 && g.M == 1 && g.ldc_n == 1) {
+                    constexpr int WG = 1024 / QG_W16_RPL, RPB = (WG / 64) * QG_W16_RPL;
+                    const size_t lds = w16_lds<F, 2>(1, g.K);
+                    hipLaunchKernelGGL((w16_gemv1r_kernel<F, WG, QG_W16_RPL>), dim3((g.N + RPB - 1) / RPB), dim3(WG), lds, st,
+                                       (const float*)g.A, (const uint8_t*)g.B, g.N, g.K, g.C);
+                    return hipGetLastError();
+                }
+                return w16_launch<F, 1, 2, 64, 1024, true>(g, st);
+            }
         return w16_launch<F, MT, 2, 64, 1024>(g, st);
+    }
+    if (QG_GEMV_SMALLK && MT <= 4 && nb % 2 == 0 && nb / 2 >= 16 && w16_lds<F, 2>(g.M < MT ? g.M : MT, g.K) <= W16_LDS_MAX) {
+        // K < 4096: 32 / 16 lanes per row, 16 rows per workgroup (as the W4A8 GEMV)
+        if (nb / 2 >= 32) {
+            if constexpr (MT == 1)
+                if (nb / 2 == 32) return w16_launch<F, 1, 2, 32, 512, true>(g, st);
+            return w16_launch<F, MT, 2, 32, 512>(g, st);
+        }
+        if constexpr (MT == 1)
+            if (nb / 2 == 16) return w16_launch<F, 1, 2, 16, 256, true>(g, st);
+        return w16_launch<F, MT, 2, 16, 256>(g, st);
     }
     if (nb % 4 == 0) {
         if (nb / 4 >= 32) return w16_launch<F, MT, 4, 32, 512>(g, st);
