@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
 #define QG_GEMV_SMALLK 1
 #endif
 #ifndef QG_W16_RPL
-#define QG_W16_RPL 1  // weight rows per wave of the M = 1 W4A16 GEMV (tuning knob; 1 = w16_gemv1_kernel)
+#define QG_W16_RPL 0  // weight rows per wave of the M = 1 W4A16 GEMV: 0 = by N (below), 1 = w16_gemv1_kernel
 #endif
 namespace {
 constexpr int W16_MT = 8;
@@ -1139,10 +1139,13 @@ template <int F, int MT> hipError_t w16_launch_mt(const GemmArgs& g, hipStream_t
         // K == 4096, Q4_0: one unit per lane (M=1 4.82 -> 4.61 us; Q8_0 measured no better)
         if constexpr (MT == 1 && F == FMT_Q4_0)
             if (nb / 2 <= 64) {
-                if (QG_W16_RPL > 1 && g.M == 1 && g.ldc_n == 1) {
-                    constexpr int WG = 1024 / QG_W16_RPL, RPB = (WG / 64) * QG_W16_RPL;
+                // two weight rows per wave from N = 8192 on (profiles/r03_tuning/r03_ab_rpl.txt: N = 11008
+                // 9.01 -> 7.73 us, N = 32000 21.3 -> 18.4; N = 4096 +1 %), bit-identical
+                constexpr int RPL = QG_W16_RPL ? QG_W16_RPL : 2;
+                if (RPL > 1 && (QG_W16_RPL || g.N >= 8192) && g.M == 1 && g.ldc_n == 1) {
+                    constexpr int WG = 1024 / RPL, RPB = (WG / 64) * RPL;
                     const size_t lds = w16_lds<F, 2>(1, g.K);
-                    hipLaunchKernelGGL((w16_gemv1r_kernel<F, WG, QG_W16_RPL>), dim3((g.N + RPB - 1) / RPB), dim3(WG), lds, st,
+                    hipLaunchKernelGGL((w16_gemv1r_kernel<F, WG, RPL>), dim3((g.N + RPB - 1) / RPB), dim3(WG), lds, st,
                                        (const float*)g.A, (const uint8_t*)g.B, g.N, g.K, g.C);
                     return hipGetLastError();
                 }

@@ -56,3 +56,17 @@ def test_small_k_grouped_bit_identical(O, qg):
     for i, n in enumerate(ns):
         single = host(qg.gemm_w4a8(a_d, b_d[i], m, n, k, t))
         assert np.array_equal(host(outs[i]).view(np.uint32), single.view(np.uint32))
+
+
+def test_w16_two_rows_per_wave_bit_identical(O, qg):
+    """M = 1 W4A16 from N = 8192 on: two weight rows per wave (w16_gemv1r_kernel) share the lane's
+    activation reads; each row keeps its summation order, so the first 4096 rows equal the one-row
+    kernel's (N = 4096) bit for bit, and all rows are within the fp32 K-term bound."""
+    n, k = 11008, 4096
+    a, b = O.fill_uniform_step4(1, n, k, seed=3)
+    bq = O.quantize(b, 2)
+    a_d, b_d = dev(a), dev(bq)
+    c_big = host(qg.gemm_w4a16(a_d, b_d, 1, n, k))
+    c_small = host(qg.gemm_w4a16(a_d, b_d[:4096].contiguous(), 1, 4096, k))
+    assert np.array_equal(c_big[:, :4096].view(np.uint32), c_small.view(np.uint32))
+    assert (np.abs(c_big.astype(np.float64) - O.gemm_w4a16(a, bq)) <= O.w16_tol(a, bq, 2)).all()
