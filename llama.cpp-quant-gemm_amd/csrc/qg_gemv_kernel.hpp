@@ -224,6 +224,7 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // constant: no A loads, no LDS, no barrier); bit 2 — no dot / epilogue (the weight dwords are summed);
 // bit 4 — nontemporal output stores; bit 8 — write-through (agent-scope, sc1) output stores;
 // bit 16 — M = 1: the workgroup's outputs gathered through LDS into one coalesced store.
+// bit 32 — output stores as agent-scope atomic exchanges (executed at the memory side: no dirty L2 lines).
 // The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
 // minimal argument list.
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL>
@@ -401,6 +402,8 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
                     if constexpr ((ABL & 4) != 0) __builtin_nontemporal_store(acc[m], C + m * ldc_m + row * ldc_n);
                     else if constexpr ((ABL & 8) != 0)
                         __hip_atomic_store(C + m * ldc_m + row * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else if constexpr ((ABL & 32) != 0)
+                        (void)__hip_atomic_exchange(C + m * ldc_m + row * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     else C[m * ldc_m + row * ldc_n] = acc[m];
                 }
         }
@@ -435,10 +438,13 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMV_WGSTORE
 #define QG_GEMV_WGSTORE 0
 #endif
+#ifndef QG_GEMV1_ABL
+#define QG_GEMV1_ABL 0  // (tuning A/B only) output-store ablation bits of the M = 1 entry, see gemv_body
+#endif
 template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
-    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, QG_GEMV_WGSTORE ? 16 : 0>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, (QG_GEMV_WGSTORE ? 16 : 0) | QG_GEMV1_ABL>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 

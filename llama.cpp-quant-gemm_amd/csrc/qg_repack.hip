@@ -117,7 +117,7 @@ hipError_t launch_repack_mfma(const GemmArgs& g, hipStream_t st) {
     const int nb = g.K / QK, nbp = g2.K / QK;
     const int rb = nb * wbytes(g.wtype), rbp = nbp * wbytes(g.wtype);
     const int ab = nb * Q8_1_BYTES, abp = nbp * Q8_1_BYTES;
-    const long wimg = round256((long)g.N * rbp), aimg = round256((long)g.M * abp);
+    const long wimg = round256((long)g.N * rbp);
     if (g.describe) {  // configuration query: the MFMA instantiation this call would run
         g2.A = reinterpret_cast<const void*>(256);
         g2.B = reinterpret_cast<const void*>(256);
