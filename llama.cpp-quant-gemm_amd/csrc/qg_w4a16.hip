@@ -32,6 +32,7 @@ template <int F, int BPL> struct w16_geom {
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 // Exact float value of weight element j (0..3) of decoded dword x: q - 8 (Q4_0), q (Q8_0).
 template <int F> __device__ __forceinline__ float w16_elem(uint32_t x, int j) {
@@ -326,6 +327,20 @@ __device__ __forceinline__ void w16_afrag(const float4 x0, const float4 x1, u32x
     }
 }
 
+// 8 fp32 activations -> two bf16 fragments, hi = RNE(a), mid = RNE(a - hi) (a - hi exact): a = hi + mid
+// + r with |r| <= 2^-16 |a| (w16s_parts: from K = 1024 on, inside the K-term bound by a factor >= 8)
+__device__ __forceinline__ void w16_afrag2(const float4 x0, const float4 x1, u32x4_t& h, u32x4_t& m) {
+    const float a[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f32x2 v = {a[2 * p], a[2 * p + 1]};
+        const uint32_t h2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+        const f32x2 r = v - f32x2{__uint_as_float(h2 << 16), __uint_as_float(h2 & 0xFFFF0000u)};  // exact
+        h[p] = h2;
+        m[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+    }
+}
+
 template <int F, int RT, int TT, int W>
 __global__ __launch_bounds__(W * 64) void w16_mfma_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                           float* __restrict__ C, int M, int N, int K, long ldc_m,
@@ -481,7 +496,7 @@ template <int F> __device__ __forceinline__ u32x4_t w16_wfrag(uint32_t x, uint32
 
 // ABL (tuning probe only; the product uses 0): 1 = each slice stores its partial tile and exits
 // (no counter, no reduction: timing of the slice work alone).
-template <int F, int RT, int TT, int KB, int ABL = 0>
+template <int F, int RT, int TT, int KB, int ABL = 0, int NP = 3>
 __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                          float* __restrict__ C, int M, int N, int K, long ldc_m,
                                                          long ldc_n, int kbs, float* __restrict__ part,
@@ -553,18 +568,19 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
         for (int j = 0; j < SJ; ++j) {
             const int it = threadIdx.x + j * RT * 64;
             u32x4_t h, mi, lo;
-            w16_afrag(x[j][0], x[j][1], h, mi, lo);
-            u32x4_t* dst = reinterpret_cast<u32x4_t*>(lds + (size_t)(it >> 6) * 3 * FR) + (it & 63);
+            if constexpr (NP == 2) w16_afrag2(x[j][0], x[j][1], h, mi);
+            else w16_afrag(x[j][0], x[j][1], h, mi, lo);
+            u32x4_t* dst = reinterpret_cast<u32x4_t*>(lds + (size_t)(it >> 6) * NP * FR) + (it & 63);
             dst[0] = h;
             dst[64] = mi;
-            dst[128] = lo;
+            if constexpr (NP == 3) dst[128] = lo;
         }
         __syncthreads();
         // 3) GB blocks at a time: operand reads + weight decode, 3 GB TT MFMAs, then the d_w epilogue
         //    (MFMA results read behind an explicit wait, as in mmq_kernel)
 #pragma unroll
         for (int g = 0; g < KB; g += GB) {
-            u32x4_t wf[GB], af[GB][TT][3];
+            u32x4_t wf[GB], af[GB][TT][NP];
             float dw[GB];
             f32x4_t c[GB][TT];
 #pragma unroll
@@ -572,10 +588,9 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
                 const int b = g + bb;
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
-                    const u32x4_t* fa = reinterpret_cast<const u32x4_t*>(lds + (size_t)(b * TT + t) * 3 * FR) + lane;
-                    af[bb][t][0] = fa[0];
-                    af[bb][t][1] = fa[64];
-                    af[bb][t][2] = fa[128];
+                    const u32x4_t* fa = reinterpret_cast<const u32x4_t*>(lds + (size_t)(b * TT + t) * NP * FR) + lane;
+#pragma unroll
+                    for (int pl = 0; pl < NP; ++pl) af[bb][t][pl] = fa[64 * pl];
                 }
                 uint32_t xl, yl, wdb;
                 if constexpr (PW) {
@@ -609,8 +624,9 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
                     const bf16x8_t wb = __builtin_bit_cast(bf16x8_t, wf[bb]);
                     f32x4_t r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][0]), wb,
                                                                         f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                    r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][1]), wb, r, 0, 0, 0);
-                    c[bb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][2]), wb, r, 0, 0, 0);
+                    if constexpr (NP == 3)
+                        r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][1]), wb, r, 0, 0, 0);
+                    c[bb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[bb][t][NP - 1]), wb, r, 0, 0, 0);
                 }
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -716,7 +732,7 @@ __global__ __launch_bounds__(RT * 64) void w16_sk_kernel(const float* __restrict
                         // VALU-bound once the split is shared; off (exact q - 8 products kept)
 #endif
 
-template <int TT, int F = FMT_Q4_0> struct w16s_geom {
+template <int TT, int F = FMT_Q4_0, int NP = 3> struct w16s_geom {
     static constexpr int ROWS = 128;              // weight rows per workgroup (4 waves x 2 tiles of 16)
     static constexpr int TOK = 16 * TT;           // tokens per workgroup
     static constexpr int BB = wfmt<F>::BB;        // 18 (Q4_0) or 34 (Q8_0): 4 blocks = 8 mod 16 bytes
@@ -731,7 +747,7 @@ template <int TT, int F = FMT_Q4_0> struct w16s_geom {
     static constexpr int SBYTES = NI * 1024;      // LDS bytes per stage
     static constexpr int AOFF = WP * 16;          // activation image offset in a stage
     static constexpr int PT = 4 * 2 * TT * 64 * 4;  // floats per partial tile (4 waves x 2 x TT tiles x 64 lanes x 4)
-    static constexpr int PLB = 3 * 4 * TT * 1024;   // activation planes of one stage ([plane][block][tt][lane] x 16 B)
+    static constexpr int PLB = NP * 4 * TT * 1024;  // activation planes of one stage ([plane][block][tt][lane] x 16 B)
     static_assert(WP + AP <= NI * 64, "stage pieces fit the DMA instructions");
 };
 
@@ -819,9 +835,9 @@ __device__ __forceinline__ void ds_write_x4_asm(uint8_t* p, u32x4_t v) {
 // (for every token tile); lane (r16, q) reads its token's 8 fp32 of k-slot q (elements 4q.. and
 // 16+4q.., two 16-B pieces of the raw image) and writes a = hi + mid + lo (truncated bf16 parts,
 // exact) as three 16-B operand fragments, planes [plane][block][tt][lane] (1 KiB each).
-template <int TT, int F>
+template <int TT, int F, int NP>
 __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, int wave, int lane) {
-    using G = w16s_geom<TT, F>;
+    using G = w16s_geom<TT, F, NP>;
     const int r16 = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
@@ -829,6 +845,23 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
         const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(ar + 16 * q);
         const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(ar + 64 + 16 * q);
         const float a[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        uint8_t* d = planes + (size_t)(wave * TT + t) * 1024 + 16 * lane;
+        if constexpr (NP == 2) {
+            // a = hi + mid + r with hi = RNE_bf16(a), mid = RNE_bf16(a - hi) (a - hi exact in f32):
+            // |r| <= 2^-16 |a| (v_cvt_pk_bf16_f32, two elements per op)
+            u32x4_t ph, pm;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t h2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a[2 * k], a[2 * k + 1]}, bf16x2_t));
+                const f32x2 hf = {__uint_as_float(h2 << 16), __uint_as_float(h2 & 0xFFFF0000u)};
+                const f32x2 r = f32x2{a[2 * k], a[2 * k + 1]} - hf;  // exact
+                ph[k] = h2;
+                pm[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+            }
+            ds_write_x4_asm(d, ph);
+            ds_write_x4_asm(d + 4 * TT * 1024, pm);
+            continue;
+        }
         uint32_t r1[8], r2[8];
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
@@ -847,7 +880,6 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
             pm[k] = hi16_pack(r1[2 * k], r1[2 * k + 1]);
             pl[k] = hi16_pack(r2[2 * k], r2[2 * k + 1]);
         }
-        uint8_t* d = planes + (size_t)(wave * TT + t) * 1024 + 16 * lane;
         ds_write_x4_asm(d, ph);
         ds_write_x4_asm(d + 4 * TT * 1024, pm);
         ds_write_x4_asm(d + 8 * TT * 1024, pl);
@@ -856,15 +888,15 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
 
 // One 4-block stage of a wave (SH: the data's byte offset in the row windows, 0 on even stages, 8
 // on odd ones). acc[i][t][e]: token 16 t + 4q + e, weight row 32 wave + 16 i + r16.
-template <int TT, int F, int SH>
+template <int TT, int F, int SH, int NP>
 __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* planes, int wave, int lane,
                                            f32x4_t (&acc)[2][TT]) {
-    using G = w16s_geom<TT, F>;
+    using G = w16s_geom<TT, F, NP>;
     constexpr bool U128 = QG_W16S_U128 && F == FMT_Q4_0;
     const int r16 = lane & 15, q = lane >> 4;
-    u32x4_t ap[3][4][TT];
+    u32x4_t ap[NP][4][TT];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NP; ++pl)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -914,7 +946,7 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
                                                                   f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
 #pragma unroll
-    for (int pl = 1; pl < 3; ++pl)
+    for (int pl = 1; pl < NP; ++pl)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -952,11 +984,11 @@ __device__ __forceinline__ void w16s_stage(const uint8_t* sb, const uint8_t* pla
 // publishes it, and every wave computes the stage. ABL (tuning probes only): 1 = DMA and waits
 // without split / compute, 2 = split + compute on whatever the LDS holds, no DMA, 3 = neither (the
 // launch, barriers and the split-K hand-off alone).
-template <int TT, int R, int ABL, int F = FMT_Q4_0>
+template <int TT, int R, int ABL, int F = FMT_Q4_0, int NP = 3>
 __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
                                                    float* __restrict__ C, int M, int N, int K, long ldc_m, long ldc_n,
                                                    int ns, float* __restrict__ part, unsigned* __restrict__ cnt) {
-    using G = w16s_geom<TT, F>;
+    using G = w16s_geom<TT, F, NP>;
     static_assert(R >= 2 && R <= 7, "ring slots (w16s_wait counts up to 7 younger stages)");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1007,12 +1039,12 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
         asm volatile("" ::: "memory");
         if (s + AHEAD < nloc) issue(s + AHEAD);  // into the slot of stage s - 1
         if constexpr (ABL != 1 && ABL != 3) {
-            w16s_split<TT, F>(slot(s), planes, wave, lane);
+            w16s_split<TT, F, NP>(slot(s), planes, wave, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // planes of stage s published
             asm volatile("" ::: "memory");
-            if ((h0 + s) & 1) w16s_stage<TT, F, 8>(slot(s), planes, wave, lane, acc);
-            else w16s_stage<TT, F, 0>(slot(s), planes, wave, lane, acc);
+            if ((h0 + s) & 1) w16s_stage<TT, F, 8, NP>(slot(s), planes, wave, lane, acc);
+            else w16s_stage<TT, F, 0, NP>(slot(s), planes, wave, lane, acc);
         }
     }
 
@@ -1248,6 +1280,15 @@ w16_plan w16_make_plan(int M, int N, int K) {
 #ifndef W16S_TT2
 #define W16S_TT2 0  // 32-token tiles for M > 16 (tuning knob)
 #endif
+#ifndef QG_W16S_NP2_MINK
+#define QG_W16S_NP2_MINK 1024  // K from which w16s_kernel splits activations into TWO bf16 parts (0: never)
+#endif
+// Activation parts of the round-2 prefill. Three truncated parts represent every fp32 activation
+// exactly; two round-to-nearest parts leave |r| <= 2^-16 |a| per element, i.e. at most
+// 2^-16 sum_k |a_k w_k| = 256 u sum_k |a_k w_k| (u = 2^-24) on an output, against the fp32 K-term
+// summation bound 2 (K + 2) u sum_k |a_k w_k| the parity tests hold the kernel to (oracle.w16_tol):
+// from K = 1024 on the representation error stays below an eighth of that bound.
+inline int w16s_parts(int K) { return QG_W16S_NP2_MINK > 0 && K >= QG_W16S_NP2_MINK ? 2 : 3; }
 w16_plan w16s_make_plan(int M, int N, int K) {
     w16_plan p;
     if (!QG_W16S || M <= 8 || M > 64 || N < 1 || K % 256 != 0) return p;
@@ -1268,32 +1309,33 @@ w16_plan w16s_make_plan(int M, int N, int K) {
     return p;
 }
 
-template <int F, int TT> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
-    using G = w16s_geom<TT, F>;
+template <int F, int TT, int NP> hipError_t w16s_launch_tt(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    using G = w16s_geom<TT, F, NP>;
     unsigned* cnt = (unsigned*)ws;
     float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
     constexpr size_t lds = (size_t)W16S_R * G::SBYTES + G::PLB;
     static_assert(lds <= 160 * 1024, "LDS per workgroup");
     static std::atomic<unsigned long long> attr_done{0};
     {
-        const hipError_t e = set_max_lds_once((const void*)w16s_kernel<TT, W16S_R, 0, F>, (int)lds, attr_done);
+        const hipError_t e = set_max_lds_once((const void*)w16s_kernel<TT, W16S_R, 0, F, NP>, (int)lds, attr_done);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0, F>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
+    hipLaunchKernelGGL((w16s_kernel<TT, W16S_R, 0, F, NP>), dim3(p.gx, p.gy, p.ks), dim3(256), lds, st, (const float*)g.A,
                        (const uint8_t*)g.B, g.C, g.M, g.N, g.K, g.ldc_m, g.ldc_n, p.ns, part, cnt);
     return hipGetLastError();
 }
 template <int F> hipError_t w16s_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
-    return p.tt == 2 ? w16s_launch_tt<F, 2>(g, p, ws, st) : w16s_launch_tt<F, 1>(g, p, ws, st);
+    if (w16s_parts(g.K) == 2) return p.tt == 2 ? w16s_launch_tt<F, 2, 2>(g, p, ws, st) : w16s_launch_tt<F, 1, 2>(g, p, ws, st);
+    return p.tt == 2 ? w16s_launch_tt<F, 2, 3>(g, p, ws, st) : w16s_launch_tt<F, 1, 3>(g, p, ws, st);
 }
 
-template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs& g, const w16_plan& p, void* ws,
-                                                                  hipStream_t st) {
+template <int F, int RT, int TT, int KB, int NP> hipError_t w16_sk_launch_np(const GemmArgs& g, const w16_plan& p, void* ws,
+                                                                          hipStream_t st) {
     const int ks = ws ? p.ks : 1;
     unsigned* cnt = (unsigned*)ws;
     float* part = ws ? (float*)((uint8_t*)ws + W16_CNT_BYTES) : nullptr;
-    constexpr size_t lds = (size_t)TT * KB * 3 * 1024;
-    auto kfn = w16_sk_kernel<F, RT, TT, KB>;
+    constexpr size_t lds = (size_t)TT * KB * NP * 1024;
+    auto kfn = w16_sk_kernel<F, RT, TT, KB, 0, NP>;
     if (lds > 64 * 1024) {
         static std::atomic<unsigned long long> attr_done{0};
         const hipError_t e = set_max_lds_once((const void*)kfn, (int)lds, attr_done);
@@ -1302,6 +1344,10 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
     hipLaunchKernelGGL(kfn, dim3(p.gx, p.gy, ks), dim3(RT * 64), lds, st, (const float*)g.A, (const uint8_t*)g.B, g.C,
                        g.M, g.N, g.K, g.ldc_m, g.ldc_n, g.K / QK / ks, part, cnt);
     return hipGetLastError();
+}
+template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs& g, const w16_plan& p, void* ws, hipStream_t st) {
+    if (w16s_parts(g.K) == 2) return w16_sk_launch_np<F, RT, TT, KB, 2>(g, p, ws, st);
+    return w16_sk_launch_np<F, RT, TT, KB, 3>(g, p, ws, st);
 }
 
 template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {

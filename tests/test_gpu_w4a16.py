@@ -90,6 +90,30 @@ def test_w16_prefill_split_k(O, qg, t, m, n, k):
     assert np.array_equal(c1, c2)
 
 
+@pytest.mark.parametrize("t", [2, 8])
+@pytest.mark.parametrize("m,n,k", [(32, 512, 4096), (16, 256, 1024), (64, 384, 2048), (24, 128, 14336),
+                                   (100, 256, 2048), (130, 300, 1024), (257, 64, 4096)])
+def test_w16_prefill_two_part_split_error(O, qg, t, m, n, k):
+    """From K = 1024 the prefill (w16s_kernel, M <= 64; w16_sk_kernel beyond) splits each activation into two round-to-nearest bf16
+    parts: |a - hi - mid| <= 2^-16 |a|. Against the exact (float64) product the error must stay within
+    that representation error plus the fp32 accumulation's (K + 2) u share, 2^-16 + (K + 2) 2^-24 of
+    sum_k |a_k w_k| (about half of the oracle-vs-kernel bound at K = 4096); a split that dropped the
+    second part (2^-8 relative) would exceed it many times over."""
+    rng = np.random.default_rng(m * 131 + k)
+    a = (rng.standard_normal((m, k)) * np.exp2(rng.integers(-6, 7, (m, 1)))).astype(np.float32)  # full 24-bit values
+    b = rng.uniform(-1, 1, (n, k)).astype(np.float32)
+    bq = O.quantize(b, t)
+    fn = qg.gemm_w4a16 if t == 2 else qg.gemm_w8a16
+    c = host(fn(dev(a), dev(bq), m, n, k)).astype(np.float64)
+    w = O.dequantize(bq, t).astype(np.float64)
+    exact = a.astype(np.float64) @ w.T
+    mag = np.abs(a.astype(np.float64)) @ np.abs(w).T
+    bound = (2.0 ** -16 + (k + 2) * 2.0 ** -24) * mag + 1e-30
+    err = np.abs(c - exact)
+    assert (err <= bound).all(), f"max err / bound {(err / bound).max()}"
+    check(O, c.astype(np.float32), a, bq, t)
+
+
 def test_w16_prefill_split_k_second_stream(O, qg):
     """Each stream gets its own workspace; results are bit-identical across streams."""
     import torch
