@@ -92,7 +92,8 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     """A BASELINE side config on this GPU the way the headline is measured: step4-recipe data,
     G launches of the product dispatch (qg_gemm_w4a8, auto) over rotating resident weight copies
     (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays.
-    forms: "single" (G launches), "batched" (one qg_gemm_w4a8_grouped launch over the G copies)."""
+    forms: "single" (G launches), "batched" (one qg_gemm_w4a8_grouped launch over the G copies),
+    "prepacked" / "padded" (the load-time padded layout), "w16" (qg_gemm_w4a16_ws: FP32 activations)."""
     wt = WTYPES[wname]
     bb = qg.BLOCK_BYTES[wt]
     a_h, b_h = qhost.fill_step4(M, N, K, 42, 0, N)
@@ -102,6 +103,11 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     c = qg.gemm_w4a8(aq, bq, M, N, K, wt)
     ref = a.double() @ b.double().T
     nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
+    af = a if "w16" in forms else None  # W4A16: the FP32 activations themselves
+    if af is not None:
+        c16 = qg.gemm_w4a16(af, bq, M, N, K)
+        nmse16 = float(torch.sum((c16.double() - ref) ** 2) / torch.sum(ref ** 2))
+        del c16
     del a, b, ref, c
     if "prepacked" in forms or "padded" in forms:  # the load-time layout for K/32 % 8 != 0 (qg_repack_weights)
         bq = qg.repack_weights(bq, N, K, wt)
@@ -129,6 +135,18 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
                                                   ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt,
                                                   ctypes.c_void_p(ws.data_ptr()), wsb, cs) != 0:
                         raise RuntimeError("qg_gemm_w4a8_prepacked failed")
+        elif form == "w16":  # qg_gemm_w4a16 with a caller workspace (the library's is never handed to a capture)
+            lib = qg._lib.load()
+            wsb = lib.qg_gemm_w16_workspace_size(M, N, K)
+            ws16 = torch.zeros(max(wsb, 16) // 4 + 64, dtype=torch.int32, device=dev)
+
+            def step() -> None:
+                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_gemm_w4a16_ws(ctypes.c_void_p(af.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
+                                            ctypes.c_void_p(out[j].data_ptr()), M, N, K, ctypes.c_void_p(ws16.data_ptr()),
+                                            wsb, cs) != 0:
+                        raise RuntimeError("qg_gemm_w4a16_ws failed")
         elif form == "padded":
             lib = qg._lib.load()
 
@@ -143,12 +161,13 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
                 qg.gemm_w4a8_grouped([aq] * G, [copies[j] for j in range(G)], [N] * G, M, K, wt,
                                      outs=[out[j] for j in range(G)])
         us = graph_time_us(step, reps, G)
-        res.append({"wtype": wname, "M": M, "N": N, "K": K, "form": form,
-                    "kernel_algo": int(qg.select_algo(M, N, K, wt)),
-                    "us_per_launch" if form in ("single", "prepacked", "padded") else "us_per_gemv": round(us, 3),
-                    "gbps": round(nbytes / us / 1e3, 1),
-                    "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
-                    "nmse_vs_fp32": nmse})
+        fb = nbytes if form != "w16" else nbytes + M * K * 4 - M * (K // 32) * 36  # FP32 activations
+        res.append({"wtype": wname if form != "w16" else wname + "_fp32_w4a16", "M": M, "N": N, "K": K, "form": form,
+                    "kernel_algo": int(qg.select_algo(M, N, K, wt)) if form != "w16" else None,
+                    "us_per_launch" if form in ("single", "prepacked", "padded", "w16") else "us_per_gemv": round(us, 3),
+                    "gbps": round(fb / us / 1e3, 1),
+                    "frac_hbm": round(fb / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
+                    "nmse_vs_fp32": nmse if form != "w16" else nmse16})
     del copies, out
     return res
 
@@ -744,7 +763,9 @@ def main() -> None:
                      ("q5_0", 1, 4096, 4096, ("single",)), ("q5_1", 1, 4096, 4096, ("single",)),
                      ("q4_0", 1, 32000, 4096, ("single", "batched")),
                      # odd K/32 at a prefill size from the load-time padded layout
-                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded"))]
+                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded")),
+                     # row f3: the W4A16 prefill (FP32 activations x Q4_0), M = 32
+                     ("q4_0", 32, 4096, 4096, ("w16",))]
             out["side_configs"] = [r for (w, m_, n_, k_, f) in sides for r in measure_config(w, m_, n_, k_, dev, forms=f)]
         print(json.dumps(out), flush=True)
     if world > 1:
