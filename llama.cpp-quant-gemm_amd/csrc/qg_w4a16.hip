@@ -1278,7 +1278,13 @@ w16_plan w16_make_plan(int M, int N, int K) {
 #define QG_W16S_Q8 1  // the round-2 prefill for W8A16 (Q8_0 weights) too
 #endif
 #ifndef W16S_TT2
-#define W16S_TT2 0  // 32-token tiles for M > 16 (tuning knob)
+#define W16S_TT2 2  // 32-token tiles: 0 never, 1 for every M > 16, 2 by the rule in w16s_make_plan
+#endif
+#ifndef W16S_MINWG
+#define W16S_MINWG 512  // split K until the grid has this many workgroups (tuning knob)
+#endif
+#ifndef W16S_MINST
+#define W16S_MINST 4  // ... keeping at least this many 4-block stages per slice (tuning knob)
 #endif
 #ifndef QG_W16S_NP2_MINK
 #define QG_W16S_NP2_MINK 1024  // K from which w16s_kernel splits activations into TWO bf16 parts (0: never)
@@ -1292,15 +1298,20 @@ inline int w16s_parts(int K) { return QG_W16S_NP2_MINK > 0 && K >= QG_W16S_NP2_M
 w16_plan w16s_make_plan(int M, int N, int K) {
     w16_plan p;
     if (!QG_W16S || M <= 8 || M > 64 || N < 1 || K % 256 != 0) return p;
-    p.tt = W16S_TT2 && M > 16 ? 2 : 1;
     p.gx = (N + 127) / 128;
+    // 32-token tiles decode each weight fragment once for two token tiles; they pay off only while the
+    // grid keeps >= 64 tiles of 128 rows x 32 tokens with no idle token rows (profiles/r03_tuning/
+    // r03_ab_w16_tt2.txt: M = 32 N = 11008 27.8 -> 23.6 us, M = 64 N = 4096 18.3 -> 17.9; slower at
+    // N = 4096 M = 24 / 32 (12.7 -> 14.8: half the tiles) and M = 48 (idle rows))
+    const bool tt2 = W16S_TT2 == 1 ? M > 16 : W16S_TT2 == 2 && M % 32 == 0 && p.gx * (M / 32) >= 64;
+    p.tt = tt2 ? 2 : 1;
     p.gy = (M + 16 * p.tt - 1) / (16 * p.tt);
     const long tiles = p.gx * p.gy;
     const int nst = K / 128;
     // >= 512 workgroups (two per CU overlap each other's barriers and LDS latency) with >= 4 stages per
     // slice (tools/w16s_probe.hip, profiles/r02_tuning/w16s_probe.txt: M=32 N=K=4096 14.3 us at 8 x 4
     // stages vs 15.8 at 4 x 8, 16.8 for the round-1 kernel)
-    int ks = (int)std::max<long>(1, std::min<long>(nst / 4, (512 + tiles - 1) / tiles));
+    int ks = (int)std::max<long>(1, std::min<long>(nst / W16S_MINST, (W16S_MINWG + tiles - 1) / tiles));
     p.ns = (nst + ks - 1) / ks;
     p.ks = (nst + p.ns - 1) / p.ns;
     if (p.ks > 1 && tiles > (long)(W16_CNT_BYTES / 4)) return w16_plan{};

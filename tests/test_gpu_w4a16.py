@@ -92,7 +92,8 @@ def test_w16_prefill_split_k(O, qg, t, m, n, k):
 
 @pytest.mark.parametrize("t", [2, 8])
 @pytest.mark.parametrize("m,n,k", [(32, 512, 4096), (16, 256, 1024), (64, 384, 2048), (24, 128, 14336),
-                                   (100, 256, 2048), (130, 300, 1024), (257, 64, 4096)])
+                                   (100, 256, 2048), (130, 300, 1024), (257, 64, 4096),
+                                   (64, 4096, 1024), (32, 8200, 2048)])  # the last two: 32-token tiles
 def test_w16_prefill_two_part_split_error(O, qg, t, m, n, k):
     """From K = 1024 the prefill (w16s_kernel, M <= 64; w16_sk_kernel beyond) splits each activation into two round-to-nearest bf16
     parts: |a - hi - mid| <= 2^-16 |a|. Against the exact (float64) product the error must stay within
