@@ -130,7 +130,10 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * (include/gemm_cuda_naive.cuh:267-274, gemm_cuda_tiled.cuh:284-291) and gemm_w8a16_naive
  * (gemm_cuda_naive.cuh:276-283); device twin of gemm_w4a16_reference (gemm_reference.h:73-112).
  * Results agree with the reference to fp32 summation order (each block's products are summed,
- * then scaled by d once). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
+ * then scaled by d once); the bf16-MFMA prefill (M > 8, K % 256 == 0) represents each activation
+ * exactly (three bf16 parts) below K = 1024 and as two round-to-nearest bf16 parts from K = 1024
+ * (added error <= 2^-16 sum_k |a_k w_k|, an eighth or less of the fp32 K-term bound
+ * 2 (K + 2) 2^-24 sum_k |a_k w_k|). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
  * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
  * call outside stream capture. Calls made during stream capture never use the library's
