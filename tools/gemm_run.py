@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one product shape L times back to back (weights rotated over > 600 MB) — a target for
 rocprofv3 kernel traces and PMC passes of the non-headline configs (e.g. the M=32 prefill,
-BASELINE configs[2]).   python tools/gemm_run.py --m 32 --n 4096 --k 4096 [--wtype 2] [--launches 200]
+BASELINE configs[2]).   python tools/gemm_run.py --m 32 --n 4096 --k 4096 [--wtype 2] [--launches 200] [--w16]
 """
 import argparse
 import ctypes
@@ -24,6 +24,7 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--wtype", type=int, default=2)
     ap.add_argument("--launches", type=int, default=200)
+    ap.add_argument("--w16", action="store_true", help="FP32 activations through qg_gemm_w4a16_ws (Q4_0) / w8a16 (Q8_0)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -37,12 +38,21 @@ def main() -> None:
     out = torch.empty((a.m, a.n), dtype=torch.float32, device=dev)
     lib = qg._lib.load()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if a.w16:
+        wsb = lib.qg_gemm_w16_workspace_size(a.m, a.n, a.k)
+        ws = torch.zeros(max(wsb, 16) // 4 + 64, dtype=torch.int32, device=dev)
+        fn = lib.qg_gemm_w4a16_ws if a.wtype == 2 else lib.qg_gemm_w8a16_ws
     for i in range(a.launches):
-        rc = lib.qg_gemm_w4a8(ctypes.c_void_p(xq.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
-                              ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)
+        if a.w16:
+            rc = fn(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                    a.m, a.n, a.k, ctypes.c_void_p(ws.data_ptr()), wsb, st)
+        else:
+            rc = lib.qg_gemm_w4a8(ctypes.c_void_p(xq.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
+                                  ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)
         assert rc == 0, rc
     torch.cuda.synchronize()
-    print(f"ok: {a.launches} launches of M={a.m} N={a.n} K={a.k} wtype={a.wtype}, algo {qg.select_algo(a.m, a.n, a.k, a.wtype)}")
+    print(f"ok: {a.launches} launches of M={a.m} N={a.n} K={a.k} wtype={a.wtype}{' W16' if a.w16 else ''}, "
+          f"algo {qg.select_algo(a.m, a.n, a.k, a.wtype)}")
 
 
 if __name__ == "__main__":
