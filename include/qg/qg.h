@@ -133,7 +133,9 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * then scaled by d once); the bf16-MFMA prefill (M > 8, K % 256 == 0) represents each activation
  * exactly (three bf16 parts) below K = 1024 and as two round-to-nearest bf16 parts from K = 1024
  * (added error <= 2^-16 sum_k |a_k w_k|, an eighth or less of the fp32 K-term bound
- * 2 (K + 2) 2^-24 sum_k |a_k w_k|). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
+ * 2 (K + 2) 2^-24 sum_k |a_k w_k|; activations of magnitude >= (2 - 2^-8) 2^127, the top 0.2 % of
+ * the float range, round to infinity there). A: 4-B aligned floats (16-B for the fast path), any
+ * K % 32 == 0.
  * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
  * call outside stream capture. Calls made during stream capture never use the library's
