@@ -2,6 +2,8 @@
 # Round-3 A/B (tuning record): W4A16 two-part split (libqg_np2.so) and the software-pipelined M <= 32
 # prefill (libqg_pipe{2,3,4}.so; libqg_base2.so = the refactored product stage), against the in-tree
 # product library; then the W4A16 GPU tests on the two-part library. Every GPU step has its own limit.
+# Kept as the record of that call: the variant libraries were built by hand (Makefile EXTRA flags,
+# -DQG_MMQ_PIPE / -DQG_MMQ_C2D from a since-reverted kernel revision) and are not kept.
 set -e
 O=gpurun_out/np2
 mkdir -p $O
