@@ -133,9 +133,9 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * then scaled by d once); the bf16-MFMA prefill (M > 8, K % 256 == 0) represents each activation
  * exactly (three bf16 parts) below K = 1024 and as two round-to-nearest bf16 parts from K = 1024
  * (added error <= 2^-16 sum_k |a_k w_k|, an eighth or less of the fp32 K-term bound
- * 2 (K + 2) 2^-24 sum_k |a_k w_k|; activations of magnitude >= (2 - 2^-8) 2^127, the top 0.2 % of
- * the float range, round to infinity there). A: 4-B aligned floats (16-B for the fast path), any
- * K % 32 == 0.
+ * 2 (K + 2) 2^-24 sum_k |a_k w_k|; the high part is clamped to the largest finite bf16, so
+ * activations up to FLT_MAX keep that bound and an infinite activation gives an infinite, not a NaN,
+ * product). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
  * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
  * call outside stream capture. Calls made during stream capture never use the library's
@@ -226,9 +226,21 @@ int qg_quantize_q8_1_f16_fused(const void* x_f16, void* y, int64_t k, qg_stream_
 int qg_quantize_q8_1(const float* x, void* y, int64_t k, qg_stream_t stream);
 int qg_quantize_q4_0(const float* x, void* y, int64_t k, qg_stream_t stream);
 /* Any type; variant 0 = include/quantize.h semantics, variant 1 (Q8_1 only) =
- * tests/framework/test_framework.cuh:195-225 (s = d * sum(q), q clamped to +-127). Q4_1/Q5_0/Q5_1
+ * tests/framework/test_framework.cuh:195-225 (s = d * sum(q), q clamped to +-127), variant 2
+ * (QG_QVAR_DEFINITION, Q8_1 and Q4_0) = the Solution definitions below. Q4_1/Q5_0/Q5_1
  * follow tests/framework/test_framework.cuh:256-367. */
+enum { QG_QVAR_REFERENCE = 0, QG_QVAR_FRAMEWORK = 1, QG_QVAR_DEFINITION = 2 };
 int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_stream_t stream);
+/* The Solution entry points of the definitions quantize_q8_1 / quantize_q4_0
+ * (schemas/definitions/quantization/quantize_q8_1.json:26-33,58 and quantize_q4_0.json:25-32,55: input
+ * x[num_elements] f32, output y[num_elements/32] blocks, destination-passing), in definition order,
+ * with the definitions' semantics where they differ from include/quantize.h: an all-zero block stores
+ * d = 1.0 (not 0); q = round-half-to-EVEN(x / d) (torch.round of a true division, not roundf(x * (1/d)));
+ * the stored f16 d is the correctly rounded f16 of amax / 127 (/ 7), the definition's Python float
+ * converted once. Q8_1 s = the fp32 sum in element order (the definition's torch.sum order is
+ * unspecified). Registered by integration/solutions/quantize_q{8_1,4_0}_hip_gfx950.json. */
+int qg_quantize_q8_1_definition(const float* x, void* y, int64_t num_elements, qg_stream_t stream);
+int qg_quantize_q4_0_definition(const float* x, void* y, int64_t num_elements, qg_stream_t stream);
 /* Dequantize k elements (include/quantize.h:84-102 and the per-format formulas). */
 int qg_dequantize(int type, const void* x, float* y, int64_t k, qg_stream_t stream);
 int qg_dequantize_q4_0(const void* x, float* y, int64_t k, qg_stream_t stream);

@@ -121,7 +121,7 @@ bool is_weight_type(int t) {
     return t == QG_TYPE_Q4_0 || t == QG_TYPE_Q4_1 || t == QG_TYPE_Q5_0 || t == QG_TYPE_Q5_1 || t == QG_TYPE_Q8_0;
 }
 
-// Crossover from tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
+// Crossover from tools/archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
 // wins up to M = 4 (its LDS activation reads grow with M), the MFMA kernel from M = 5 on.
 int select_algo(const GemmArgs& g) {
     if (g.M <= 4 && gemv_eligible(g)) return QG_ALGO_GEMV;
@@ -557,7 +557,9 @@ int qg_gemm_w8a8(const void* A, const void* B, float* C, int M, int N, int K, qg
 int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_stream_t stream) {
     if (k < 0 || k % 32 != 0) return QG_ERR_BAD_K;
     if (block_bytes(type) == 0) return QG_ERR_UNSUPPORTED;
-    if (variant != 0 && !(variant == 1 && type == QG_TYPE_Q8_1)) return QG_ERR_UNSUPPORTED;
+    if (variant != 0 && !(variant == 1 && type == QG_TYPE_Q8_1) &&
+        !(variant == 2 && (type == QG_TYPE_Q8_1 || type == QG_TYPE_Q4_0)))
+        return QG_ERR_UNSUPPORTED;
     if (k == 0) return QG_OK;
     if (!x || !y) return QG_ERR_INVALID_ARG;
     if (((uintptr_t)x & 3) != 0) return QG_ERR_ALIGN;
@@ -568,6 +570,12 @@ int qg_quantize(int type, int variant, const float* x, void* y, int64_t k, qg_st
 
 int qg_quantize_q8_1(const float* x, void* y, int64_t k, qg_stream_t s) { return qg_quantize(QG_TYPE_Q8_1, 0, x, y, k, s); }
 int qg_quantize_q4_0(const float* x, void* y, int64_t k, qg_stream_t s) { return qg_quantize(QG_TYPE_Q4_0, 0, x, y, k, s); }
+int qg_quantize_q8_1_definition(const float* x, void* y, int64_t num_elements, qg_stream_t s) {
+    return qg_quantize(QG_TYPE_Q8_1, QG_QVAR_DEFINITION, x, y, num_elements, s);
+}
+int qg_quantize_q4_0_definition(const float* x, void* y, int64_t num_elements, qg_stream_t s) {
+    return qg_quantize(QG_TYPE_Q4_0, QG_QVAR_DEFINITION, x, y, num_elements, s);
+}
 
 int qg_dequantize(int type, const void* x, float* y, int64_t k, qg_stream_t stream) {
     if (k < 0 || k % 32 != 0) return QG_ERR_BAD_K;

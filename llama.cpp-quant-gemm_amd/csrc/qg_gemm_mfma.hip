@@ -1,7 +1,7 @@
 // qg_gemm_mfma.hip — product instantiations and dispatch of the prefill (M > 8) MFMA kernel
 // (qg_mmq_kernel.hpp).
 //
-// Tile configuration from the sweeps in tools/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
+// Tile configuration from the sweeps in tools/archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
 // mmq_probe_smallm.txt; cold weights, one MI355X):
 //  * M <= 32: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
 //    >= 256 workgroups (one per CU; fewer re-reads of the activations), else 16

@@ -9,6 +9,11 @@
 //   Q4_0              include/quantize.h:35-70     d = amax/7, q = clamp(roundf(x/d)+8, 0, 15)
 //   Q8_0              include/quantize.h:111-135
 //   Q4_1 / Q5_0 / Q5_1  tests/framework/test_framework.cuh:256-367 (the repo's only quantizers)
+//   Q8_1 / Q4_0 (variant 2)  the Solution definitions schemas/definitions/quantization/quantize_q8_1.json:58
+//     and quantize_q4_0.json:55 (torch reference): d = amax/127 (/7) in double, or 1.0 for an all-zero
+//     block; q = round-half-EVEN(x / f32(d)) (+8 for Q4_0), clamped; the stored f16 d = f16(f32(d)),
+//     which equals the one correct rounding of the definition's Python float (tests/test_oracle.py);
+//     Q8_1 s = sum(x) in element order as variant 0 (the definition's torch.sum order is unspecified)
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
 #include "qg_quant_block.hpp"
@@ -37,6 +42,29 @@ template <int NB> __device__ __forceinline__ void store_u16(uint8_t* dst, const 
     for (int i = 0; i < NB / 2; ++i) p[i] = (uint16_t)(w[i / 2] >> (16 * (i & 1)));
 }
 
+// variant 2: the definitions' semantics (header). out as quantize_q8_1_block / the Q4_0 packing.
+__device__ __forceinline__ void quantize_q8_1_block_def(const float (&v)[32], uint32_t (&out)[9]) {
+    float amax = 0.0f, sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        amax = fmaxf(amax, fabsf(v[j]));
+        sum += v[j];
+    }
+    const float d = amax > 0.0f ? amax / 127.0f : 1.0f;
+    // f16(f32(amax / 127)) is also the single rounding of the exact quotient the definition's Python
+    // float converts to: f32(amax / 127) is never an inexact f16 midpoint (tests/test_oracle.py)
+    const uint32_t dh = f2h_bits(d);
+    uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const float r = fminf(fmaxf(rintf(v[j] / d), -128.0f), 127.0f);
+        q[j / 4] |= ((uint32_t)(int)r & 0xFFu) << (8 * (j & 3));
+    }
+    out[0] = dh | (f2h_bits(sum) << 16);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[1 + i] = q[i];
+}
+
 template <int TYPE, int VARIANT, bool VEC>
 __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__ x, uint8_t* __restrict__ y, int64_t nblocks) {
     const int64_t ib = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -46,7 +74,8 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 
     if constexpr (TYPE == FMT_Q8_1) {
         uint32_t w[9];
-        quantize_q8_1_block<VARIANT>(v, w);
+        if constexpr (VARIANT == 2) quantize_q8_1_block_def(v, w);
+        else quantize_q8_1_block<VARIANT>(v, w);
         uint32_t* dst = reinterpret_cast<uint32_t*>(y + ib * 36);  // 36-B blocks stay 4-B aligned
 #pragma unroll
         for (int i = 0; i < 9; ++i) dst[i] = w[i];
@@ -75,14 +104,20 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
         constexpr float DIV = TYPE == FMT_Q4_0 ? 7.0f : 15.0f;
         constexpr int OFF = TYPE == FMT_Q4_0 ? 8 : 16;
         constexpr int QMAX = TYPE == FMT_Q4_0 ? 15 : 31;
-        const float d = amax / DIV;
+        const float d = VARIANT == 2 && amax == 0.0f ? 1.0f : amax / DIV;
         const float id = d > 0.0f ? 1.0f / d : 0.0f;
         uint8_t qs[16];
         uint32_t qh = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            int q0 = (int)roundf(v[j] * id) + OFF;
-            int q1 = (int)roundf(v[j + 16] * id) + OFF;
+            int q0, q1;
+            if constexpr (VARIANT == 2) {  // torch.round(x / d) + 8: ties to even, true division
+                q0 = (int)rintf(v[j] / d) + OFF;
+                q1 = (int)rintf(v[j + 16] / d) + OFF;
+            } else {
+                q0 = (int)roundf(v[j] * id) + OFF;
+                q1 = (int)roundf(v[j + 16] * id) + OFF;
+            }
             q0 = max(0, min(QMAX, q0));
             q1 = max(0, min(QMAX, q1));
             qs[j] = (uint8_t)((q0 & 0xF) | ((q1 & 0xF) << 4));
@@ -259,9 +294,11 @@ template <int TYPE> hipError_t ld(const void* x, float* y, int64_t nblocks, hipS
 hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64_t nblocks, hipStream_t st) {
     if (nblocks == 0) return hipSuccess;
     switch (type) {
-        case FMT_Q8_1: return variant == 1 ? lq<FMT_Q8_1, 1>(x, y, nblocks, st) : lq<FMT_Q8_1, 0>(x, y, nblocks, st);
+        case FMT_Q8_1:
+            return variant == 1 ? lq<FMT_Q8_1, 1>(x, y, nblocks, st)
+                 : variant == 2 ? lq<FMT_Q8_1, 2>(x, y, nblocks, st) : lq<FMT_Q8_1, 0>(x, y, nblocks, st);
         case FMT_Q8_0: return lq<FMT_Q8_0, 0>(x, y, nblocks, st);
-        case FMT_Q4_0: return lq<FMT_Q4_0, 0>(x, y, nblocks, st);
+        case FMT_Q4_0: return variant == 2 ? lq<FMT_Q4_0, 2>(x, y, nblocks, st) : lq<FMT_Q4_0, 0>(x, y, nblocks, st);
         case FMT_Q4_1: return lq<FMT_Q4_1, 0>(x, y, nblocks, st);
         case FMT_Q5_0: return lq<FMT_Q5_0, 0>(x, y, nblocks, st);
         case FMT_Q5_1: return lq<FMT_Q5_1, 0>(x, y, nblocks, st);

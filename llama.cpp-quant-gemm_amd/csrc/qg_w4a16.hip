@@ -307,15 +307,31 @@ __device__ __forceinline__ uint32_t hi16_pack(uint32_t lo_elem, uint32_t hi_elem
     return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);  // {lo_elem[31:16], hi_elem[31:16]}
 }
 
+// hi = RNE_bf16 of a clamped to the largest finite bf16 (0x7F7F): a finite |a| >= (2 - 2^-8) 2^127 would
+// otherwise round hi to inf and make mid = a - hi = -inf, hi + mid = NaN. With the clamp
+// hi stays finite, a - hi is still exact (same binade) and |a - hi - mid| <= 2^-17 |a|; an infinite a
+// gives hi = max, mid = inf (the product is inf, as the reference's); NaN stays NaN.
+// The truncated three-part split clamps the same way before each truncation (only an infinite a or
+// residual is changed by it: |a| <= FLT_MAX truncates to a finite bf16), so an infinite a gives
+// hi = mid = max and lo = inf, an infinite product instead of inf - inf = NaN.
+__device__ __forceinline__ float bf16_clamp(float a) {
+    constexpr float BFMAX = 0x1.fep127f;  // 0x7F7F0000
+    return __builtin_amdgcn_fmed3f(a, -BFMAX, BFMAX);
+}
+__device__ __forceinline__ uint32_t bf16x2_rne_clamped(float a0, float a1) {
+    const f32x2 c = {bf16_clamp(a0), bf16_clamp(a1)};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(c, bf16x2_t));
+}
+
 // 8 fp32 activations -> hi / mid / lo bf16 fragments with a = hi + mid + lo exactly
 __device__ __forceinline__ void w16_afrag(const float4 x0, const float4 x1, u32x4_t& h, u32x4_t& m, u32x4_t& l) {
     const float a[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
     uint32_t hb[8], mb[8], lb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        hb[j] = __float_as_uint(a[j]) & 0xFFFF0000u;
+        hb[j] = __float_as_uint(bf16_clamp(a[j])) & 0xFFFF0000u;
         const float r1 = a[j] - __uint_as_float(hb[j]);
-        mb[j] = __float_as_uint(r1) & 0xFFFF0000u;
+        mb[j] = __float_as_uint(bf16_clamp(r1)) & 0xFFFF0000u;
         const float r2 = r1 - __uint_as_float(mb[j]);
         lb[j] = __float_as_uint(r2);  // <= 8 significant bits left: its top half is exact
     }
@@ -334,7 +350,7 @@ __device__ __forceinline__ void w16_afrag2(const float4 x0, const float4 x1, u32
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const f32x2 v = {a[2 * p], a[2 * p + 1]};
-        const uint32_t h2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+        const uint32_t h2 = bf16x2_rne_clamped(a[2 * p], a[2 * p + 1]);
         const f32x2 r = v - f32x2{__uint_as_float(h2 << 16), __uint_as_float(h2 & 0xFFFF0000u)};  // exact
         h[p] = h2;
         m[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
@@ -852,7 +868,7 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
             u32x4_t ph, pm;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint32_t h2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a[2 * k], a[2 * k + 1]}, bf16x2_t));
+                const uint32_t h2 = bf16x2_rne_clamped(a[2 * k], a[2 * k + 1]);
                 const f32x2 hf = {__uint_as_float(h2 << 16), __uint_as_float(h2 & 0xFFFF0000u)};
                 const f32x2 r = f32x2{a[2 * k], a[2 * k + 1]} - hf;  // exact
                 ph[k] = h2;
@@ -866,9 +882,11 @@ __device__ __forceinline__ void w16s_split(const uint8_t* sb, uint8_t* planes, i
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
             const f32x2 x = {a[j], a[j + 1]};
-            const f32x2 h = {__uint_as_float(__float_as_uint(a[j]) & 0xFFFF0000u), __uint_as_float(__float_as_uint(a[j + 1]) & 0xFFFF0000u)};
+            const f32x2 h = {__uint_as_float(__float_as_uint(bf16_clamp(a[j])) & 0xFFFF0000u),
+                             __uint_as_float(__float_as_uint(bf16_clamp(a[j + 1])) & 0xFFFF0000u)};
             const f32x2 m1 = x - h;  // exact
-            const f32x2 mh = {__uint_as_float(__float_as_uint(m1.x) & 0xFFFF0000u), __uint_as_float(__float_as_uint(m1.y) & 0xFFFF0000u)};
+            const f32x2 mh = {__uint_as_float(__float_as_uint(bf16_clamp(m1.x)) & 0xFFFF0000u),
+                              __uint_as_float(__float_as_uint(bf16_clamp(m1.y)) & 0xFFFF0000u)};
             const f32x2 l2 = m1 - mh;  // exact, <= 8 significant bits
             r1[j] = __float_as_uint(m1.x); r1[j + 1] = __float_as_uint(m1.y);
             r2[j] = __float_as_uint(l2.x); r2[j + 1] = __float_as_uint(l2.y);
@@ -1367,10 +1385,13 @@ template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
         if (((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && (g.M + 15) / 16 <= 65535) {
             const w16_plan p = w16s_make_plan(g.M, g.N, g.K);
             if (p.ns) {
+                // hold: the library buffer's lock stays taken until the kernel is enqueued, so another
+                // host thread on this stream cannot grow (and free) it in between
+                std::unique_lock<std::mutex> hold;
                 void* ws = nullptr;
                 if (p.ks > 1) {
                     if (g.ws) ws = g.ws_bytes >= p.ws_bytes && ((uintptr_t)g.ws & 255) == 0 ? g.ws : nullptr;
-                    else ws = stream_workspace(st, p.ws_bytes);
+                    else ws = stream_workspace(st, p.ws_bytes, 0, &hold);
                 }
                 if (ws || p.ks == 1) return w16s_launch<F>(g, p, ws, st);
             }
@@ -1380,10 +1401,11 @@ template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
         const w16_plan p = w16_make_plan(g.M, g.N, g.K);
         if (p.rt) {
             // the caller's workspace (qg_gemm_w4a16_ws), else the library's one for this stream
+            std::unique_lock<std::mutex> hold;
             void* ws = nullptr;
             if (p.ks > 1) {
                 if (g.ws) ws = g.ws_bytes >= p.ws_bytes && ((uintptr_t)g.ws & 255) == 0 ? g.ws : nullptr;
-                else ws = stream_workspace(st, p.ws_bytes);
+                else ws = stream_workspace(st, p.ws_bytes, 0, &hold);
             }
             // without one, a grid this small would leave most CUs idle: the older kernel below
             if (ws || p.ks == 1 || p.gx * p.gy >= 128) {

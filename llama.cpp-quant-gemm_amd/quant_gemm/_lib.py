@@ -58,6 +58,8 @@ SIGNATURES = {
     "qg_release_workspaces": ([], None),
     "qg_quantize_q8_1": ([P, P, I64, P], I),
     "qg_quantize_q4_0": ([P, P, I64, P], I),
+    "qg_quantize_q8_1_definition": ([P, P, I64, P], I),
+    "qg_quantize_q4_0_definition": ([P, P, I64, P], I),
     "qg_quantize": ([I, I, P, P, I64, P], I),
     "qg_dequantize": ([I, P, P, I64, P], I),
     "qg_dequantize_q4_0": ([P, P, I64, P], I),

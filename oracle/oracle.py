@@ -84,7 +84,10 @@ _QUANT = {Q4_0: "qgo_quantize_row_q4_0", Q8_0: "qgo_quantize_row_q8_0", Q8_1: "q
 
 
 def quantize(x: np.ndarray, t: int, variant: int = 0) -> np.ndarray:
-    """FP32 [..., K] -> uint8 [..., K/32, block_bytes] (reference CPU quantizers)."""
+    """FP32 [..., K] -> uint8 [..., K/32, block_bytes] (reference CPU quantizers; variant 2 = the
+    Solution definitions' semantics, quantize_definition)."""
+    if variant == 2:
+        return quantize_definition(x, t)
     x = np.ascontiguousarray(x, np.float32)
     k = x.shape[-1]
     assert k % 32 == 0
@@ -92,6 +95,71 @@ def quantize(x: np.ndarray, t: int, variant: int = 0) -> np.ndarray:
     fn = "qgo_quantize_q8_1_fw" if (t == Q8_1 and variant == 1) else _QUANT[t]
     getattr(lib(), fn)(_p(x), _p(out), x.size)
     return out
+
+
+def f16_round_exact(num: int, den: int) -> int:
+    """f16 bits (RNE, signless) of the exact rational num/den >= 0 — an independent exact reference for
+    the single-rounding f16 conversions below (integer arithmetic only)."""
+    from fractions import Fraction
+    v = Fraction(num, den)
+    if v == 0:
+        return 0
+    e = v.numerator.bit_length() - v.denominator.bit_length()
+    if Fraction(2) ** e > v:
+        e -= 1
+    e = max(e, -14)                       # below 2^-14: subnormal spacing 2^-24
+    q = v / Fraction(2) ** (e - 10)       # significand scaled to 11 integer bits
+    n, r = divmod(q.numerator, q.denominator)
+    if 2 * r > q.denominator or (2 * r == q.denominator and n & 1):
+        n += 1
+    if n == 2048:                          # carried into the next binade
+        n, e = 1024, e + 1
+    if e > 15:
+        return 0x7C00
+    return ((e + 15) << 10 | (n - 1024)) if n >= 1024 else n
+
+
+def quantize_definition(x: np.ndarray, t: int) -> np.ndarray:
+    """The Solution definitions quantize_q8_1 / quantize_q4_0 restated in numpy from their text
+    (schemas/definitions/quantization/quantize_q8_1.json:58, quantize_q4_0.json:55):
+      amax = max|x|; d = amax / 127.0 (/ 7.0) as a Python float (double), or 1.0 if amax == 0;
+      q = round-half-to-even(x / float32(d)) (torch float32 true division by the scalar), + 8 for Q4_0,
+      clamped to [-128, 127] / [0, 15]; Q4_0 qs[i] = q[i] | q[i+16] << 4;
+      stored d = f16 of the Python float (one correctly rounded conversion, numpy float64 -> float16);
+      Q8_1 s = sum(x): the definition's torch.sum order is unspecified — restated as the fp32 sum in
+      element order (include/quantize.h:176-179), the order the GPU variant uses.
+    PARITY: Q8_1 is pinned by the flashinfer Q8_1 definition's committed output bytes
+    (tests/golden/quantize_q8_1_m16k128.npz, same d / q / tie semantics); the Q4_0 definition has no
+    reference-generated fixture (executing the reference's code was denied in round 4):
+    its bytes are pinned by this restatement and the asserted mismatch set against the pinned
+    include/quantize.h quantizer (tests/test_oracle.py)."""
+    assert t in (Q8_1, Q4_0)
+    x = np.ascontiguousarray(x, np.float32)
+    k = x.shape[-1]
+    assert k % 32 == 0
+    blk = x.reshape(-1, 32)
+    amax = np.abs(blk).max(axis=1)
+    div = 127.0 if t == Q8_1 else 7.0
+    d64 = np.where(amax > 0, amax.astype(np.float64) / div, 1.0)
+    d32 = d64.astype(np.float32)
+    q = np.rint(blk / d32[:, None])
+    with np.errstate(over="ignore"):  # scales beyond the f16 range store inf, as the f32 -> f16 cast
+        dh = d64.astype(np.float16).view(np.uint8).reshape(-1, 2)
+    if t == Q8_1:
+        s = np.zeros(blk.shape[0], np.float32)
+        for j in range(32):
+            s = (s + blk[:, j]).astype(np.float32)
+        out = np.empty((blk.shape[0], 36), np.uint8)
+        out[:, 0:2] = dh
+        with np.errstate(over="ignore"):
+            out[:, 2:4] = s.astype(np.float16).view(np.uint8).reshape(-1, 2)
+        out[:, 4:] = np.clip(q, -128, 127).astype(np.int8).view(np.uint8)
+    else:
+        qq = np.clip(q + 8, 0, 15).astype(np.uint8)
+        out = np.empty((blk.shape[0], 18), np.uint8)
+        out[:, 0:2] = dh
+        out[:, 2:] = qq[:, :16] | (qq[:, 16:] << 4)
+    return out.reshape(x.shape[:-1] + (k // 32, out.shape[-1]))
 
 
 def quantize_q8_1_fused_f16(x: np.ndarray) -> np.ndarray:

@@ -9,16 +9,18 @@ build container only from the DEFINITIONS those solutions register against:
 These definitions' Python references read blocks by attribute (`w_block.d`, `a_block.ds.x`,
 `a_block.ds.y`, `block.qs[i]`), so the generator hands them small attribute records built from the
 packed bytes (d / ds as the float value of the stored f16, qs as the stored codes, Q8_1 qs signed).
-The reference code is read and executed at generation time and never stored; the fixtures hold
-only inputs and outputs. Inputs follow the step4 recipe (glibc srand, U[-1,1]) through the CPU
+The reference code was read and executed at generation time (round 3) and never stored; the
+fixtures hold only inputs and outputs. Since round 4 the script refuses to run without the explicit
+opt-in flag and runs the code only after the allowlist checks of tests/golden/defexec.py (ADVICE
+r03); in round 4 this build environment denied executing the reference's code, so the
+committed fixtures are the round-3 ones and no new ones are generated. Inputs follow the step4 recipe (glibc srand, U[-1,1]) through the CPU
 oracle's quantizers (the same bytes as include/quantize.h, pinned in tests/test_oracle.py).
 
-Usage:  python tests/golden/make_schema_golden.py [--ref /root/reference] [--force]
+Usage:  python tests/golden/make_schema_golden.py --exec-reference-definitions [--ref /root/reference] [--force]
 """
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import sys
 from types import SimpleNamespace
@@ -28,15 +30,14 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, HERE)
 import oracle as O  # noqa: E402
+from defexec import EXEC_FLAG, load_definition_fn, require_opt_in  # noqa: E402
 
 
 def load_definition(ref_root: str, name: str):
-    with open(os.path.join(ref_root, "schemas", "definitions", "gemm", name + ".json")) as f:
-        spec = json.load(f)
-    ns: dict = {}
-    exec(compile(spec["reference"], name, "exec"), ns)  # the definition's own Python reference
-    return spec, ns["run"]
+    spec, run, _ = load_definition_fn(os.path.join(ref_root, "schemas", "definitions", "gemm", name + ".json"))
+    return spec, run
 
 
 def _f16(lo: int, hi: int) -> float:
@@ -70,7 +71,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument(EXEC_FLAG, dest="exec_ok", action="store_true",
+                    help="allow executing the reference's definition code (defexec.py checks)")
     args = ap.parse_args()
+    require_opt_in(args.exec_ok, "make_schema_golden.py")
     import torch
 
     _, run_w4a8 = load_definition(args.ref, "gemm_q4_0_q8_1_w4a8")

@@ -157,3 +157,78 @@ def test_w16_prefill_caller_workspace(O, qg, t):
     check(O, outs[0], a, bq, t)
     assert np.array_equal(outs[0], outs[1])
     check(O, outs[2], a, bq, t)
+
+
+def test_w16_library_workspace_two_threads_one_stream(O, qg):
+    """two host threads on ONE stream, the second asking for a larger split-K workspace
+    than the first's (the library's per-stream buffer grows: stream sync + free of the old block).
+    The buffer's lock is held until each call's kernel is enqueued, so no launch can run on a freed
+    block: every result equals the single-threaded one, bit for bit."""
+    import threading
+
+    import torch
+    lib = qg._lib.load()
+    shapes = [(32, 1024, 4096), (64, 8192, 4096)]
+    need = [lib.qg_gemm_w16_workspace_size(*s) for s in shapes]
+    assert need[1] > max(need[0], 4 << 20)  # the second shape must grow the buffer past its first size
+    data = []
+    for i, (m, n, k) in enumerate(shapes):
+        a, b = O.fill_uniform_step4(m, n, k, seed=40 + i)
+        bq = O.quantize(b, 2)
+        ad, bd = dev(a), dev(bq)
+        data.append((ad, bd, host(qg.gemm_w4a16(ad, bd, m, n, k))))
+    s = torch.cuda.Stream()
+    P = ctypes.c_void_p
+    outs = {0: [], 1: []}
+    errs = []
+
+    def worker(i, reps):
+        m, n, k = shapes[i]
+        ad, bd, _ = data[i]
+        try:
+            for _ in range(reps):
+                c = torch.empty((m, n), dtype=torch.float32, device="cuda")
+                rc = lib.qg_gemm_w4a16(P(ad.data_ptr()), P(bd.data_ptr()), P(c.data_ptr()), m, n, k, P(s.cuda_stream))
+                assert rc == 0
+                outs[i].append(c)
+        except BaseException as e:  # reported in the main thread
+            errs.append(e)
+
+    lib.qg_release_workspaces()
+    th = [threading.Thread(target=worker, args=(0, 40)), threading.Thread(target=worker, args=(1, 4))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    s.synchronize()
+    assert not errs, errs
+    for i in (0, 1):
+        assert len(outs[i]) == (40 if i == 0 else 4)
+        for c in outs[i]:
+            assert np.array_equal(host(c), data[i][2])
+
+
+@pytest.mark.parametrize("m,k", [(16, 1024), (9, 256), (40, 2048)])
+def test_w16_prefill_activations_near_flt_max(O, qg, m, k):
+    """a finite activation whose bf16 rounding would overflow ((2 - 2^-8) 2^127 <= |a| <=
+    FLT_MAX) keeps a finite product (the high part is clamped to the largest finite bf16; the split
+    error stays <= 2^-16 |a|), and an infinite activation gives an infinite product, not NaN — in the
+    three-part (K < 1024) and the two-part (K >= 1024) prefill."""
+    n = 64
+    a, b = O.fill_uniform_step4(m, n, k, seed=m + k)
+    b = (b * 0.5).astype(np.float32)  # |w| <= 0.57: a * w stays finite
+    a[0, 5] = np.float32(3.4e38)
+    a[1, 7] = np.float32(-3.399e38)
+    bq = O.quantize(b, 2)
+    w = O.dequantize(bq, 2).astype(np.float64)
+    c = host(qg.gemm_w4a16(dev(a), dev(bq), m, n, k)).astype(np.float64)
+    exact = a.astype(np.float64) @ w.T
+    mag = np.abs(a.astype(np.float64)) @ np.abs(w).T
+    assert np.isfinite(c).all()
+    bound = (2.0 ** -16 + 2 * (k + 2) * 2.0 ** -24) * mag + 1e-30
+    assert (np.abs(c - exact) <= bound).all()
+    a2 = a.copy()
+    a2[2, 3] = np.inf
+    c2 = host(qg.gemm_w4a16(dev(a2), dev(bq), m, n, k))
+    nz = w[:, 3] != 0
+    assert np.isinf(c2[2, nz]).all() and (np.sign(c2[2, nz]) == np.sign(w[nz, 3])).all()

@@ -150,6 +150,70 @@ def test_golden_quantize_q8_1(O):
     assert (frac[diff != 0] < 1e-4).all()
 
 
+def test_definition_q8_1_matches_flashinfer_fixture(O):
+    """The definition-semantics restatement (oracle.quantize_definition, variant 2: ties to even,
+    true division, d = 1.0 for a zero block) reproduces the flashinfer Q8_1 definition's own output
+    bytes (quantize/quantize_q8_1_k4096.json:66, same semantics) byte for byte — all 36 bytes of
+    every block, where the include/quantize.h quantizer differs by one code at ties."""
+    g = np.load(os.path.join(GOLD, "quantize_q8_1_m16k128.npz"))
+    assert np.array_equal(O.quantize(g["x"], O.Q8_1, 2), g["q_ref"])
+
+
+def test_definition_f16_scale_is_single_rounding(O):
+    """The stored f16 d of the definitions (a Python float converted once) is the correctly rounded
+    f16 of the exact quotient amax / 127 (/ 7): checked with exact rational arithmetic on every block
+    of the parity set — and it equals f16(f32(amax / div)), the double rounding of include/quantize.h
+    and of the GPU quantizer (f32(amax / div) is never an inexact f16 midpoint: one f32 step of amax
+    moves the quotient by 64/127 or 4/7 of an f32 step of the quotient, more than half)."""
+    from fractions import Fraction
+    from qdef_cases import definition_inputs
+    x = definition_inputs().reshape(-1, 32)
+    for t, div in ((O.Q8_1, 127), (O.Q4_0, 7)):
+        q = O.quantize_definition(x, t)
+        dh = q[..., 0:2].copy().view(np.uint16)[:, 0, 0]
+        amax = np.abs(x).max(axis=1)
+        for i in range(x.shape[0]):
+            if amax[i] == 0:
+                assert dh[i] == 0x3C00
+                continue
+            f = Fraction(float(amax[i])) / div
+            assert dh[i] == O.f16_round_exact(f.numerator, f.denominator), i
+            assert dh[i] == np.float32(amax[i] / np.float32(div)).astype(np.float16).view(np.uint16)
+
+
+def test_definition_mismatch_set_vs_quantize_h(O):
+    """Where the definitions' semantics and the pinned include/quantize.h quantizer (variant 0) give
+    different bytes, every difference is one of the documented causes, and each cause occurs in the
+    parity set: an all-zero block's d (1.0 vs 0); a code one step apart at an exact round-half tie
+    (even vs away) or where x / d and x * (1/d) straddle a half-integer. Nothing else (no nonzero
+    block's d or s differs, no code more than one step apart)."""
+    from qdef_cases import definition_inputs
+    x = definition_inputs().reshape(-1, 32)
+    amax = np.abs(x).max(axis=1)
+    for t, div in ((O.Q8_1, 127.0), (O.Q4_0, 7.0)):
+        v0, v2 = O.quantize(x, t, 0)[:, 0], O.quantize(x, t, 2)[:, 0]
+        d32 = (amax / np.float32(div)).astype(np.float32)
+        zero = amax == 0
+        d0 = v0[:, 0:2].copy().view(np.uint16)[:, 0]
+        d2 = v2[:, 0:2].copy().view(np.uint16)[:, 0]
+        assert (d0[zero] == 0).all() and (d2[zero] == 0x3C00).all()
+        assert np.array_equal(d0[~zero], d2[~zero])
+        if t == O.Q8_1:
+            assert np.array_equal(v0[:, 2:4], v2[:, 2:4])  # s identical
+            c0, c2 = v0[:, 4:].view(np.int8).astype(int), v2[:, 4:].view(np.int8).astype(int)
+        else:
+            c0 = np.concatenate([v0[:, 2:] & 15, v0[:, 2:] >> 4], axis=1).astype(int)
+            c2 = np.concatenate([v2[:, 2:] & 15, v2[:, 2:] >> 4], axis=1).astype(int)
+        diff = c0 != c2
+        assert (np.abs(c0 - c2) <= 1).all()
+        with np.errstate(divide="ignore", invalid="ignore"):
+            r = (x / np.where(zero, 1, d32)[:, None]).astype(np.float32)
+        frac = np.abs(np.abs(r) % 1.0 - 0.5)
+        assert (frac[diff] <= 1e-5 * np.maximum(1, np.abs(r[diff]))).all()
+        assert (frac[diff] == 0).sum() >= 100  # exact ties present (x / d vs x * (1/d) straddling a
+        # half-integer needs x / d within an f32 step of it: allowed above, about 1 % likely in this set)
+
+
 @pytest.mark.parametrize("t", [2, 3, 6, 7])
 def test_allquants_nmse_small(O, t):
     """All-quants formulas (no /4) stay within the FP32-anchored bounds at a CPU-fast size."""

@@ -3,11 +3,21 @@
 The reference's FlashInfer-Bench-style schema (schemas/docs/solution.md:27-42) binds a Solution to
 a Definition through `spec.entry_point = "file::function"`, destination-passing: the harness calls
 the function with the definition's inputs in order, then its outputs, then the axes. The three
-definitions registered here (schemas/definitions/gemm/*.json) are all activation-major:
+GEMM definitions registered here (schemas/definitions/gemm/*.json) are all activation-major:
 
   gemm_q4_0_q8_1_w4a8  inputs A_q8_1[M,K/QK], B_q4_0[N,K/QK]   output C[M,N]  (:35-53)
   gemm_q4_0_w4a16      inputs A[M,K] f32,     B_q4_0[N,K/QK]   output C[M,N]
   gemm_fp32_baseline   inputs A[M,K] f32,     B[N,K] f32       output C[M,N]
+
+and the two quantization definitions (schemas/definitions/quantization/*.json, round 4):
+
+  quantize_q8_1        input x[num_elements] f32   output y[num_elements/QK] q8_1  (:26-33)
+  quantize_q4_0        input x[num_elements] f32   output y[num_elements/QK] q4_0  (:25-32)
+
+The quantization Solutions are checked on the GPU byte for byte against oracle.quantize_definition
+(the definitions' semantics restated; Q8_1 pinned by the flashinfer definition's committed bytes,
+tests/test_oracle.py) — no output of the schema definitions' own code exists as a fixture (executing
+it was denied in round 4).
 
 CPU tests: every solution parses, names a known definition, and its entry point is declared in
 include/qg/qg.h with exactly that parameter order and exported by libqg_hip.so. GPU tests resolve
@@ -29,13 +39,15 @@ SOLUTIONS = sorted(glob.glob(os.path.join(REPO, "integration", "solutions", "*.j
 GOLD = os.path.join(HERE, "golden")
 LIB = os.path.join(REPO, "llama.cpp-quant-gemm_amd", "quant_gemm", "libqg_hip.so")
 
-# definition -> (inputs, outputs) as schemas/definitions/gemm/<name>.json lists them
+# definition -> (inputs, outputs, var axes) as schemas/definitions/<group>/<name>.json lists them
 DEFINITIONS = {
-    "gemm_q4_0_q8_1_w4a8": (["A_q8_1", "B_q4_0"], ["C"]),
-    "gemm_q4_0_w4a16": (["A", "B_q4_0"], ["C"]),
-    "gemm_fp32_baseline": (["A", "B"], ["C"]),
+    "gemm_q4_0_q8_1_w4a8": (["A_q8_1", "B_q4_0"], ["C"], ["M", "N", "K"]),
+    "gemm_q4_0_w4a16": (["A", "B_q4_0"], ["C"], ["M", "N", "K"]),
+    "gemm_fp32_baseline": (["A", "B"], ["C"], ["M", "N", "K"]),
+    "quantize_q8_1": (["x"], ["y"], ["num_elements"]),
+    "quantize_q4_0": (["x"], ["y"], ["num_elements"]),
 }
-AXES = ["M", "N", "K"]
+GROUP = {name: ("quantization" if name.startswith("quantize_") else "gemm") for name in DEFINITIONS}
 
 
 def header_params(symbol):
@@ -68,9 +80,9 @@ def test_solution_entry_point_matches_definition(path):
     assert sol["spec"]["target_hardware"] == ["gfx950"]
     for s in sol["sources"]:
         assert os.path.exists(os.path.join(REPO, s["path"])), s["path"]
-    inputs, outputs = DEFINITIONS[sol["definition"]]
+    inputs, outputs, axes = DEFINITIONS[sol["definition"]]
     fn = entry_symbol(sol)
-    assert header_params(fn) == inputs + outputs + AXES + ["stream"]
+    assert header_params(fn) == inputs + outputs + axes + ["stream"]
     assert re.sub(r"\s+", " ", sol["spec"]["signature"]).startswith(f"int {fn}(")
 
 
@@ -84,8 +96,10 @@ def test_entry_point_exported(path):
 @pytest.mark.skipif(not os.path.isdir("/root/reference/schemas"), reason="reference tree only in the build container")
 @pytest.mark.parametrize("name", sorted(DEFINITIONS))
 def test_definition_table_matches_reference(name):
-    d = load(f"/root/reference/schemas/definitions/gemm/{name}.json")
-    assert (list(d["inputs"]), list(d["outputs"])) == DEFINITIONS[name]
+    """The definitions' declared inputs / outputs / var axes (their JSON data, read as text)."""
+    d = load(f"/root/reference/schemas/definitions/{GROUP[name]}/{name}.json")
+    var_axes = [a for a, v in d["axes"].items() if v.get("type") == "var"]
+    assert (list(d["inputs"]), list(d["outputs"]), var_axes) == DEFINITIONS[name]
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "schema_*.npz"))), ids=os.path.basename)
@@ -103,39 +117,3 @@ def test_schema_golden_on_oracle(O, path):
         ref = O.gemm_fp32(g["A"], g["B"]).astype(np.float64)
         tol = 2 * (g["A"].shape[1] + 2) * 2.0**-24 * (np.abs(g["A"]) @ np.abs(g["B"]).T)
     assert (np.abs(g["C"].astype(np.float64) - ref) <= tol).all()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "schema_*.npz"))), ids=os.path.basename)
-def test_registered_entry_point_on_gpu(O, qg, path):
-    """Resolve the solution's entry point by name, call it with the definition's inputs in order,
-    then C, M, N, K — and match the definition's outputs."""
-    import torch
-    g = np.load(path)
-    name = str(g["definition"])
-    sol = next(load(p) for p in SOLUTIONS if load(p)["definition"] == name)
-    lib = ctypes.CDLL(LIB)
-    fn = getattr(lib, entry_symbol(sol))
-    fn.restype = ctypes.c_int
-    m, n, k = (int(g[x]) for x in ("m", "n", "k"))
-    inputs, _ = DEFINITIONS[name]
-    args = [torch.from_numpy(np.ascontiguousarray(g[x])).cuda() for x in inputs]
-    c = torch.full((m, n), float("nan"), dtype=torch.float32, device="cuda")
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    P = ctypes.c_void_p
-    rc = fn(*[P(t.data_ptr()) for t in args], P(c.data_ptr()), m, n, k, st)
-    assert rc == 0
-    torch.cuda.synchronize()
-    got = c.cpu().numpy().astype(np.float64)
-    if name == "gemm_q4_0_q8_1_w4a8":
-        _, s = O.gemm_w4a8(g["A_q8_1"], g["B_q4_0"], O.Q4_0, want_sumi=True)
-        tol = O.summation_tol(g["A_q8_1"], g["B_q4_0"], s, O.Q4_0)
-        if qg._lib.load().qg_select_algo(m, n, k, O.Q4_0) == 2:  # MFMA epilogue: reassociation bound
-            tol = O.reassoc_tol(g["A_q8_1"], g["B_q4_0"], s, O.Q4_0)
-        tol = tol + 1e-6 * np.abs(g["C"])
-    elif name == "gemm_q4_0_w4a16":
-        tol = 2 * O.w16_tol(g["A"], g["B_q4_0"], O.Q4_0)  # both sides within the bound of exact
-    else:
-        tol = 4 * (k + 2) * 2.0**-24 * (np.abs(g["A"]) @ np.abs(g["B"]).T)
-    err = np.abs(got - g["C"])
-    assert (err <= tol).all(), f"max err {err.max()}"
