@@ -1,0 +1,143 @@
+// qg_shard.hip — libqg_shard.so: row-sharded multi-GPU W4A8 product over RCCL (include/qg/qg_shard.h).
+//
+// One rank per GPU (process or thread), the caller's communicator. Per call, on the caller's stream:
+//   1. the rank's rows through libqg_hip.so (qg_gemm_w4a8_ldc, QG_ALGO_AUTO) into its slice of the
+//      gather buffer — C itself when M == 1 and N % G == 0 (in-place all-gather), else the
+//      [G][M][P] workspace (P = ceil(N / G) rows per rank, equal slices: ONE collective);
+//   2. ncclAllGather of the M * P floats (in place: sendbuff = recvbuff + rank * count);
+//   3. (workspace form) one reorder kernel [G][M][P] -> C[M][N], dropping the padded columns.
+// Nothing else crosses the links: the rows are independent, so there is no exchange
+// step. The single-GPU library does not link RCCL; this one does (-lrccl), and calls it only here.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "qg/qg_shard.h"
+
+namespace {
+
+thread_local int g_last_nccl = 0;
+
+int nccl_status(ncclResult_t r) {
+    if (r == ncclSuccess) return QG_OK;
+    g_last_nccl = (int)r;
+    return QG_ERR_HIP;
+}
+
+inline long per_rank(int N, int world) { return ((long)N + world - 1) / world; }
+
+// recv [G][M][P] -> C[M][N]: C[m][g P + j] = recv[g][m][j] for g P + j < N (coalesced along j)
+__global__ __launch_bounds__(256) void shard_reorder_kernel(const float* __restrict__ recv, float* __restrict__ C, int M,
+                                                            int N, int P) {
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;  // over M * N outputs, n fastest
+    if (idx >= (long)M * N) return;
+    const int m = (int)(idx / N), n = (int)(idx - (long)m * N);
+    const int g = n / P, j = n - g * P;
+    C[idx] = recv[((long)g * M + m) * P + j];
+}
+
+}  // namespace
+
+extern "C" {
+
+int qg_shard_rows(int N, int world, int rank, int* row0, int* rows) {
+    if (N < 0 || world < 1 || rank < 0 || rank >= world || !row0 || !rows) return QG_ERR_INVALID_ARG;
+    const long P = per_rank(N, world);
+    const long r0 = std::min<long>((long)rank * P, N);
+    *row0 = (int)r0;
+    *rows = (int)std::min<long>(P, N - r0);
+    return QG_OK;
+}
+
+size_t qg_sharded_gemm_workspace_size(int M, int N, int world) {
+    if (M <= 0 || N <= 0 || world < 1) return 0;
+    if (M == 1 && N % world == 0) return 0;
+    return (size_t)world * (size_t)M * (size_t)per_rank(N, world) * sizeof(float);
+}
+
+int qg_sharded_gemm_w4a8_local(const void* A, const void* B_shard, float* C_slice, int M, int N, int K, int wtype,
+                               int world, int rank, qg_stream_t stream) {
+    int row0 = 0, rows = 0;
+    const int rc = qg_shard_rows(N, world, rank, &row0, &rows);
+    if (rc != QG_OK) return rc;
+    if (M < 0) return QG_ERR_INVALID_ARG;
+    if (M == 0 || rows == 0) return QG_OK;  // an empty shard leaves its (padding) slice untouched
+    return qg_gemm_w4a8_ldc(A, B_shard, C_slice, M, rows, K, per_rank(N, world), wtype, QG_ALGO_AUTO, stream);
+}
+
+int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, int N, int K, int wtype, void* ws,
+                         size_t ws_bytes, qg_nccl_comm_t comm, qg_stream_t stream) {
+    if (!comm) return QG_ERR_INVALID_ARG;
+    if (M < 0 || N < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (M == 0 || N == 0) return QG_OK;
+    if (!A || !C) return QG_ERR_INVALID_ARG;
+    int world = 0, rank = 0;
+    if (nccl_status(ncclCommCount((ncclComm_t)comm, &world)) != QG_OK) return QG_ERR_HIP;
+    if (nccl_status(ncclCommUserRank((ncclComm_t)comm, &rank)) != QG_OK) return QG_ERR_HIP;
+    int row0 = 0, rows = 0;
+    qg_shard_rows(N, world, rank, &row0, &rows);
+    if (rows > 0 && !B_shard) return QG_ERR_INVALID_ARG;
+    const long P = per_rank(N, world);
+    const size_t count = (size_t)M * (size_t)P;
+    hipStream_t st = (hipStream_t)stream;
+    const bool in_place = M == 1 && N % world == 0;
+    float* recv = C;
+    if (!in_place) {
+        const size_t need = qg_sharded_gemm_workspace_size(M, N, world);
+        if (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0) return QG_ERR_UNSUPPORTED;
+        recv = static_cast<float*>(ws);
+    }
+    float* mine = recv + (size_t)rank * count;
+    int rc = qg_sharded_gemm_w4a8_local(A, B_shard, mine, M, N, K, wtype, world, rank, stream);
+    if (rc != QG_OK) return rc;
+    rc = nccl_status(ncclAllGather(mine, recv, count, ncclFloat32, (ncclComm_t)comm, st));
+    if (rc != QG_OK) return rc;
+    if (!in_place) {
+        const long total = (long)M * N;
+        hipLaunchKernelGGL(shard_reorder_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                           (const float*)recv, C, M, N, (int)P);
+        if (hipGetLastError() != hipSuccess) return QG_ERR_HIP;
+    }
+    return QG_OK;
+}
+
+int qg_shard_get_unique_id(void* id128) {
+    if (!id128) return QG_ERR_INVALID_ARG;
+    static_assert(sizeof(ncclUniqueId) == QG_NCCL_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const int rc = nccl_status(ncclGetUniqueId(&id));
+    if (rc == QG_OK) memcpy(id128, &id, sizeof(id));
+    return rc;
+}
+
+int qg_shard_comm_init_rank(qg_nccl_comm_t* comm, int world, const void* id128, int rank) {
+    if (!comm || !id128 || world < 1 || rank < 0 || rank >= world) return QG_ERR_INVALID_ARG;
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof(id));
+    ncclComm_t c = nullptr;
+    const int rc = nccl_status(ncclCommInitRank(&c, world, id, rank));
+    *comm = rc == QG_OK ? (qg_nccl_comm_t)c : nullptr;
+    return rc;
+}
+
+int qg_shard_comm_destroy(qg_nccl_comm_t comm) {
+    if (!comm) return QG_ERR_INVALID_ARG;
+    return nccl_status(ncclCommDestroy((ncclComm_t)comm));
+}
+
+int qg_shard_comm_count(qg_nccl_comm_t comm, int* world) {
+    if (!comm || !world) return QG_ERR_INVALID_ARG;
+    return nccl_status(ncclCommCount((ncclComm_t)comm, world));
+}
+
+int qg_shard_comm_rank(qg_nccl_comm_t comm, int* rank) {
+    if (!comm || !rank) return QG_ERR_INVALID_ARG;
+    return nccl_status(ncclCommUserRank((ncclComm_t)comm, rank));
+}
+
+int qg_shard_last_nccl_error(void) { return g_last_nccl; }
+
+}  // extern "C"

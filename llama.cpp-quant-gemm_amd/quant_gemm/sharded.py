@@ -114,3 +114,124 @@ class RowShardedW4A8:
         g = self.gather_buffer(M)
         self.gather(out, g)
         return self.assemble(g, self.n_total)
+
+
+# ---------------------------------------------------------------------------------------------
+# Native path: libqg_shard.so (include/qg/qg_shard.h) — the rank's kernel and ONE ncclAllGather
+# over the caller's RCCL communicator, stream-ordered inside the C library (what a C++ caller such as
+# llama.cpp links). The communicator is created here from a 128-byte RCCL unique id that rank 0 makes
+# and the process group broadcasts (gloo or nccl); the GEMM call itself never creates one.
+_shard_lib = None
+
+
+def shard_lib():
+    """ctypes handle of libqg_shard.so (next to libqg_hip.so); raises if it is not built."""
+    global _shard_lib
+    if _shard_lib is None:
+        import ctypes
+        import os
+
+        from . import _lib as L
+        L.load()  # libqg_hip.so first: libqg_shard.so resolves it next to itself
+        path = os.path.join(L.HERE, "libqg_shard.so")
+        if not os.path.exists(path):
+            raise ImportError(f"quant_gemm: {path} not built; run `make -C {L.CSRC}`")
+        lib = ctypes.CDLL(path)
+        P, I, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        sig = {
+            "qg_shard_rows": ([I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)], I),
+            "qg_sharded_gemm_workspace_size": ([I, I, I], SZ),
+            "qg_sharded_gemm_w4a8": ([P, P, P, I, I, I, I, P, SZ, P, P], I),
+            "qg_sharded_gemm_w4a8_local": ([P, P, P, I, I, I, I, I, I, P], I),
+            "qg_shard_get_unique_id": ([P], I),
+            "qg_shard_comm_init_rank": ([ctypes.POINTER(P), I, P, I], I),
+            "qg_shard_comm_destroy": ([P], I),
+            "qg_shard_comm_count": ([P, ctypes.POINTER(I)], I),
+            "qg_shard_comm_rank": ([P, ctypes.POINTER(I)], I),
+            "qg_shard_last_nccl_error": ([], I),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes, fn.restype = args, res
+        _shard_lib = lib
+    return _shard_lib
+
+
+def native_shard_rows(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """qg_shard_rows through the C-ABI, as [start, stop) (== shard_rows)."""
+    import ctypes
+    r0, rows = ctypes.c_int(), ctypes.c_int()
+    rc = shard_lib().qg_shard_rows(n_total, world, rank, ctypes.byref(r0), ctypes.byref(rows))
+    if rc != 0:
+        raise RuntimeError(f"qg_shard_rows: status {rc}")
+    return r0.value, r0.value + rows.value
+
+
+class NcclComm:
+    """An RCCL communicator made by the caller-side harness: rank 0's unique id is broadcast over
+    ``group`` (any backend), then every rank joins with qg_shard_comm_init_rank on its current
+    device. ``close()`` destroys it."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None):
+        import ctypes
+        lib = shard_lib()
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            rc = lib.qg_shard_get_unique_id(ctypes.c_void_p(uid.data_ptr()))
+            if rc != 0:
+                raise RuntimeError(f"ncclGetUniqueId failed (ncclResult {lib.qg_shard_last_nccl_error()})")
+        if world > 1:
+            src = uid.cuda() if dist.get_backend(group) == "nccl" else uid
+            dist.broadcast(src, 0, group=group)
+            uid = src.cpu()
+        comm = ctypes.c_void_p()
+        rc = lib.qg_shard_comm_init_rank(ctypes.byref(comm), world, ctypes.c_void_p(uid.data_ptr()), rank)
+        if rc != 0:
+            raise RuntimeError(f"ncclCommInitRank failed (ncclResult {lib.qg_shard_last_nccl_error()})")
+        self.handle, self.world, self.rank = comm, world, rank
+
+    def close(self) -> None:
+        if self.handle:
+            shard_lib().qg_shard_comm_destroy(self.handle)
+            self.handle = None
+
+
+class NativeRowShardedW4A8:
+    """C[M, N] = A_q8_1[M, K] . B[N, K]^T through libqg_shard.so: this rank's rows (shard_rows) in
+    ``weight_q_local``; ``forward`` returns the full C on every rank (one native all-gather)."""
+
+    def __init__(self, weight_q_local: torch.Tensor, n_total: int, K: int, comm: NcclComm, wtype: int = 2):
+        self.comm, self.n_total, self.K, self.wtype = comm, n_total, K, wtype
+        self.start, self.stop = native_shard_rows(n_total, comm.world, comm.rank)
+        if weight_q_local.shape[0] != self.stop - self.start:
+            raise RuntimeError(f"rank {comm.rank}: expected {self.stop - self.start} weight rows, "
+                               f"got {weight_q_local.shape[0]}")
+        self.weight = weight_q_local.contiguous()
+        self._ws = None
+
+    def workspace(self, M: int) -> Optional[torch.Tensor]:
+        need = shard_lib().qg_sharded_gemm_workspace_size(M, self.n_total, self.comm.world)
+        if need == 0:
+            return None
+        if self._ws is None or self._ws.numel() * 4 < need:
+            self._ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.weight.device)
+        return self._ws
+
+    def forward(self, act_q: torch.Tensor, M: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        import ctypes
+        dev = self.weight.device
+        if out is None:
+            out = torch.empty((M, self.n_total), dtype=torch.float32, device=dev)
+        ws = self.workspace(M)
+        P = ctypes.c_void_p
+        st = P(torch.cuda.current_stream(dev).cuda_stream)
+        with torch.cuda.device(dev):
+            rc = shard_lib().qg_sharded_gemm_w4a8(
+                P(act_q.data_ptr()), P(self.weight.data_ptr() if self.weight.numel() else 0), P(out.data_ptr()),
+                M, self.n_total, self.K, self.wtype, P(ws.data_ptr() if ws is not None else 0),
+                0 if ws is None else ws.numel() * 4, self.comm.handle, st)
+        if rc != 0:
+            raise RuntimeError(f"qg_sharded_gemm_w4a8: status {rc} (ncclResult {shard_lib().qg_shard_last_nccl_error()})")
+        return out

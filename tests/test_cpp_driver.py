@@ -29,3 +29,26 @@ def test_cpp_driver_runs(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def build_shard(tmp_path):
+    exe = str(tmp_path / "test_shard")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17",
+                    "-I", os.path.join(REPO, "include"), os.path.join(REPO, "tests", "cpp", "test_shard.cpp"),
+                    "-L", LIBDIR, "-lqg_shard", "-lqg_hip", "-lrccl", "-pthread",
+                    f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+    return exe
+
+
+def test_cpp_shard_driver_compiles(tmp_path):
+    """The native multi-GPU caller (one RCCL communicator per device, libqg_shard.so) links cleanly."""
+    assert os.path.exists(build_shard(tmp_path))
+
+
+@pytest.mark.gpu
+def test_cpp_shard_driver_runs(tmp_path):
+    """World = the visible GPUs (1 on the test box): every rank's full C vs single-GPU qg_gemm_w4a8."""
+    exe = build_shard(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr

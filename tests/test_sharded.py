@@ -115,3 +115,57 @@ def test_row_sharded_group_gather_gloo(world, m, n, k):
     for rank, cs, refs in res:
         for c, ref in zip(cs, refs):
             assert c.shape == (m, n) and np.array_equal(c, ref)
+
+
+# ------------------------------------------------------------------ native path (libqg_shard.so)
+SHARD_HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "qg", "qg_shard.h")
+
+
+def shard_declared():
+    import re
+    src = re.sub(r"/\*.*?\*/", "", open(SHARD_HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(qg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_native_shard_library_exports_header():
+    """libqg_shard.so (RCCL) loads without a GPU and exports every function qg_shard.h declares;
+    the ctypes table binds exactly those."""
+    import subprocess
+    import re
+    from quant_gemm import sharded
+    lib = sharded.shard_lib()
+    fns = shard_declared()
+    assert "qg_sharded_gemm_w4a8" in fns and "qg_shard_comm_init_rank" in fns
+    for f in fns:
+        assert hasattr(lib, f), f
+    path = os.path.join(os.path.dirname(sharded.__file__), "libqg_shard.so")
+    nm = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    assert set(fns) <= set(re.findall(r" T (qg_\w+)", nm))
+    need = subprocess.run(["readelf", "-d", path], capture_output=True, text=True, check=True).stdout
+    assert "librccl" in need and "libqg_hip.so" in need
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 4097, 32000, 32001])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_native_shard_rows_match_python(n, world):
+    from quant_gemm import sharded
+    for r in range(world):
+        assert sharded.native_shard_rows(n, world, r) == sharded.shard_rows(n, world, r)
+
+
+def test_native_shard_validation_without_launch():
+    """Status codes returned before any HIP / RCCL call (no GPU needed)."""
+    import ctypes
+    from quant_gemm import sharded
+    lib = sharded.shard_lib()
+    P = ctypes.c_void_p
+    a = (ctypes.c_uint8 * 64)()
+    rc = lib.qg_sharded_gemm_w4a8(P(ctypes.addressof(a)), P(ctypes.addressof(a)), P(ctypes.addressof(a)), 1, 8, 64,
+                                  2, None, 0, None, None)
+    assert rc == -1  # no communicator
+    assert lib.qg_shard_rows(10, 0, 0, ctypes.byref(ctypes.c_int()), ctypes.byref(ctypes.c_int())) == -1
+    assert lib.qg_shard_rows(10, 2, 2, ctypes.byref(ctypes.c_int()), ctypes.byref(ctypes.c_int())) == -1
+    assert lib.qg_sharded_gemm_workspace_size(1, 32000, 8) == 0          # in place
+    assert lib.qg_sharded_gemm_workspace_size(1, 32001, 8) == 8 * 4001 * 4
+    assert lib.qg_sharded_gemm_workspace_size(3, 4096, 2) == 2 * 3 * 2048 * 4
+    assert lib.qg_shard_comm_init_rank(None, 1, None, 0) == -1
