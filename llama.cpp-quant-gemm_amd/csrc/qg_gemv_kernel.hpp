@@ -462,10 +462,13 @@ template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     constexpr int RPB = (WGS / 64) * (64 / LPR);
     const GemvItemDesc d = grp.it[blockIdx.y];
-    if ((int)blockIdx.x * RPB >= d.N) return;  // past this item's rows (uniform)
+    // the single launch's XCD-aware tile order (gemv_body) within the item: with grid.x a multiple of 8
+    // the workgroup's XCD is blockIdx.x % 8, so each XCD takes a contiguous range of the item's tiles
+    const int tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    if (tile * RPB >= d.N) return;  // past this item's rows (uniform)
     gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, 0>(
         reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K, d.C, 0,
-        d.ldc, 1, nullptr, (int)blockIdx.x);
+        d.ldc, 1, nullptr, tile);
 }
 
 // Host side -------------------------------------------------------------------------------------

@@ -211,15 +211,20 @@ def test_w16_library_workspace_two_threads_one_stream(O, qg):
 @pytest.mark.parametrize("m,k", [(16, 1024), (9, 256), (40, 2048)])
 def test_w16_prefill_activations_near_flt_max(O, qg, m, k):
     """a finite activation whose bf16 rounding would overflow ((2 - 2^-8) 2^127 <= |a| <=
-    FLT_MAX) keeps a finite product (the high part is clamped to the largest finite bf16; the split
-    error stays <= 2^-16 |a|), and an infinite activation gives an infinite product, not NaN — in the
-    three-part (K < 1024) and the two-part (K >= 1024) prefill."""
-    n = 64
-    a, b = O.fill_uniform_step4(m, n, k, seed=m + k)
-    b = (b * 0.5).astype(np.float32)  # |w| <= 0.57: a * w stays finite
+    FLT_MAX) keeps a finite product — the high part is clamped to the largest finite bf16 (before the
+    clamp: hi = inf, mid = -inf, NaN) — and an infinite activation gives an infinite product, not NaN,
+    in the three-part (K < 1024) and the two-part (K >= 1024) prefill. The kernels form each block's
+    code dot sum a * (q - 8) before scaling by d, so the weights here keep |q - 8| <= 1 (every partial
+    product then stays below FLT_MAX, as the reference's a * w does)."""
+    rng = np.random.default_rng(m * 3 + k)
+    n, nb = 64, k // 32
+    a, _ = O.fill_uniform_step4(m, n, k, seed=m + k)
     a[0, 5] = np.float32(3.4e38)
     a[1, 7] = np.float32(-3.399e38)
-    bq = O.quantize(b, 2)
+    bq = np.zeros((n, nb, 18), np.uint8)
+    bq[..., 0:2] = rng.uniform(1e-3, 0.1, (n, nb)).astype(np.float16).view(np.uint8).reshape(n, nb, 2)
+    codes = rng.integers(7, 10, (n, nb, 32)).astype(np.uint8)  # q - 8 in {-1, 0, 1}
+    bq[..., 2:] = codes[..., :16] | (codes[..., 16:] << 4)
     w = O.dequantize(bq, 2).astype(np.float64)
     c = host(qg.gemm_w4a16(dev(a), dev(bq), m, n, k)).astype(np.float64)
     exact = a.astype(np.float64) @ w.T
@@ -231,4 +236,5 @@ def test_w16_prefill_activations_near_flt_max(O, qg, m, k):
     a2[2, 3] = np.inf
     c2 = host(qg.gemm_w4a16(dev(a2), dev(bq), m, n, k))
     nz = w[:, 3] != 0
+    assert nz.sum() > 10
     assert np.isinf(c2[2, nz]).all() and (np.sign(c2[2, nz]) == np.sign(w[nz, 3])).all()
