@@ -396,6 +396,83 @@ def sharded_leg(mods, aq, M: int, G: int, rows: int, world: int, steps: int, war
     return {"us_per_gemv": round(elapsed / (steps * G) * 1e6, 3), "launch_stream_us_per_gemv": round(launch_us, 3)}
 
 
+def native_leg(wc, aq, M: int, G: int, n_total: int, K: int, wt: int, world: int, steps: int, warmup: int, dev) -> dict:
+    """The same strong-scaling step through the native C path (libqg_shard.so, include/qg/qg_shard.h):
+    per step G local products (qg_sharded_gemm_w4a8_local: the rank's kernel, captured as a hipGraph)
+    and ONE qg_shard_all_gather_f32 of the step's [G, M, P] slices over an RCCL communicator the
+    harness creates (quant_gemm.sharded.NcclComm) on a side stream, double-buffered so the gather of
+    step i overlaps step i + 1's kernels — what a C++ caller of the library does."""
+    import ctypes
+
+    from quant_gemm.sharded import NcclComm, shard_lib
+    lib = shard_lib()
+    comm = NcclComm()
+    P = ctypes.c_void_p
+    rows = rows_per_rank(n_total, world)
+    R = wc.shape[0]
+    outs = [torch.zeros((G, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world, G, M, rows), dtype=torch.float32, device=dev) for _ in range(2)]
+    gs = torch.cuda.Stream()
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    computed = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def step(s: int) -> None:
+        st = P(torch.cuda.current_stream().cuda_stream)
+        for j in range(G):
+            rc = lib.qg_sharded_gemm_w4a8_local(P(aq.data_ptr()), P(wc[j % R].data_ptr()), P(outs[s][j].data_ptr()),
+                                                M, n_total, K, wt, world, comm.rank, st)
+            assert rc == 0, rc
+
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        step(0)
+        step(1)
+    torch.cuda.synchronize()
+    graphs = []
+    for s in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step(s)
+        graphs.append(g)
+    started = [False, False]
+
+    def run(i: int) -> None:
+        s = i % 2
+        if started[s]:
+            torch.cuda.current_stream().wait_event(done[s])  # the gather that read outs[s] two steps ago
+        graphs[s].replay()
+        computed[s].record()
+        gs.wait_event(computed[s])
+        rc = lib.qg_shard_all_gather_f32(P(outs[s].data_ptr()), P(gathered[s].data_ptr()), outs[s].numel(), comm.handle,
+                                         P(gs.cuda_stream))
+        assert rc == 0, rc
+        done[s].record(gs)
+        started[s] = True
+
+    try:
+        for i in range(warmup):
+            run(i)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            run(i)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # every rank's gathered step equals its own slices where they are its rows (spot check)
+        ok = bool(torch.equal(gathered[(steps - 1) % 2][comm.rank], outs[(steps - 1) % 2]))
+    finally:
+        del graphs
+        comm.close()
+    return {"us_per_gemv": round(elapsed / (steps * G) * 1e6, 3), "own_slice_roundtrip_ok": ok,
+            "path": "libqg_shard.so: qg_sharded_gemm_w4a8_local x G (hipGraph) + qg_shard_all_gather_f32 (RCCL) per step"}
+
+
 def strong_legs(world: int, rank: int, dev, G: int, steps: int, warmup: int, M: int = 1, K: int = 4096,
                 n_total: int = 32000, wname: str = "q4_0") -> dict:
     """BASELINE configs[4] as STRONG scaling: the N=32000 GEMV split over the ranks, both legs, and
@@ -413,17 +490,27 @@ def strong_legs(world: int, rank: int, dev, G: int, steps: int, warmup: int, M: 
     mods = [RowShardedW4A8(wc[i], n_total, K, wt) for i in range(R)]
     legs = {form: sharded_leg(mods, aq, M, G, rows, world, steps, warmup, form, dev)
             for form in ("per_launch", "batched")}
+    # the native C path (libqg_shard.so over its own RCCL communicator): one rank per GPU only (RCCL
+    # refuses two ranks on one device, so the gloo rehearsal skips it); reported, never fatal
+    if dist.get_backend() != "nccl":
+        legs["native"] = {"skipped": f"needs one GPU per rank over RCCL (backend {dist.get_backend()})"}
+    else:
+        try:
+            legs["native"] = native_leg(wc, aq, M, G, n_total, K, wt, world, steps, warmup, dev)
+        except Exception as e:  # noqa: BLE001
+            legs["native"] = {"error": f"{type(e).__name__}: {e}"}
     del mods, wc
     torch.cuda.empty_cache()
     one = measure_config(wname, M, n_total, K, dev, G, forms=("single", "batched"))
     one_single = one[0]["us_per_launch"]
     one_batched = one[1]["us_per_gemv"]
     return {"config": f"{wname} M={M} N={n_total} K={K}: {rows} rows per GPU x {world} GPUs, all-gather per step of {G}",
-            "per_launch": legs["per_launch"], "batched": legs["batched"],
+            "per_launch": legs["per_launch"], "batched": legs["batched"], "native": legs["native"],
             "one_gpu_n32000": {"single_us_per_launch": one_single, "batched_us_per_gemv": one_batched},
             "strong_speedup_vs_1gpu_n32000": {
                 "per_launch": round(one_single / legs["per_launch"]["us_per_gemv"], 3),
                 "batched": round(one_batched / legs["batched"]["us_per_gemv"], 3),
+                "native": (round(one_single / legs["native"]["us_per_gemv"], 3) if "us_per_gemv" in legs["native"] else None),
                 "note": "1-GPU us per GEMV / N-GPU us per GEMV (wall clock per step incl. the all-gather, max over "
                         "ranks), like for like per leg; DESIGN.md §7"}}
 

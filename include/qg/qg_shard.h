@@ -59,6 +59,11 @@ int qg_sharded_gemm_w4a8(const void* A_q8_1, const void* B_shard, float* C, int 
 int qg_sharded_gemm_w4a8_local(const void* A_q8_1, const void* B_shard, float* C_slice, int M, int N, int K,
                                int wtype, int world, int rank, qg_stream_t stream);
 
+/* One ncclAllGather of `count` floats per rank (recv = world * count floats, rank-major; in place when
+ * send == recv + rank * count) on `stream` — the gather of a step of several local products at once
+ * (e.g. G independent GEMVs' [G][M][P] slices written by qg_sharded_gemm_w4a8_local). */
+int qg_shard_all_gather_f32(const float* send, float* recv, size_t count, qg_nccl_comm_t comm, qg_stream_t stream);
+
 /* Caller-side conveniences over RCCL (ncclGetUniqueId / ncclCommInitRank / ncclCommDestroy) for
  * callers without RCCL headers: the 128-byte id is created on one rank and broadcast by the caller. */
 enum { QG_NCCL_UNIQUE_ID_BYTES = 128 };

@@ -104,6 +104,12 @@ int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, in
     return QG_OK;
 }
 
+int qg_shard_all_gather_f32(const float* send, float* recv, size_t count, qg_nccl_comm_t comm, qg_stream_t stream) {
+    if (!comm || !send || !recv) return QG_ERR_INVALID_ARG;
+    if (count == 0) return QG_OK;
+    return nccl_status(ncclAllGather(send, recv, count, ncclFloat32, (ncclComm_t)comm, (hipStream_t)stream));
+}
+
 int qg_shard_get_unique_id(void* id128) {
     if (!id128) return QG_ERR_INVALID_ARG;
     static_assert(sizeof(ncclUniqueId) == QG_NCCL_UNIQUE_ID_BYTES, "ncclUniqueId size");

@@ -143,6 +143,7 @@ def shard_lib():
             "qg_sharded_gemm_workspace_size": ([I, I, I], SZ),
             "qg_sharded_gemm_w4a8": ([P, P, P, I, I, I, I, P, SZ, P, P], I),
             "qg_sharded_gemm_w4a8_local": ([P, P, P, I, I, I, I, I, I, P], I),
+            "qg_shard_all_gather_f32": ([P, P, SZ, P, P], I),
             "qg_shard_get_unique_id": ([P], I),
             "qg_shard_comm_init_rank": ([ctypes.POINTER(P), I, P, I], I),
             "qg_shard_comm_destroy": ([P], I),

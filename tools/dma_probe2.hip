@@ -87,6 +87,46 @@ __global__ __launch_bounds__(LW * 64) void dma2_kernel(const uint8_t* __restrict
     if (lane == 0 && K < 0) sink[blockIdx.x] = (float)smem[wave];
 }
 
+// Linear order: a row tile's weights (BN consecutive rows = ONE contiguous BN * RB-byte region) and a
+// token tile's activations (NT consecutive rows, contiguous too) moved as lane-linear 1-KB pieces in
+// address order (ORDER 0), or the weights chunk-major (ORDER 1: the 1-KB chunk c of every row before
+// chunk c + 1 — the order a consumer working along K needs), LW waves taking pieces round-robin.
+// MODE as above. LDS destinations wrap at 144 KB (movement only).
+template <int BN, int NT, int LW, int ORDER, int MODE, int CP>
+__global__ __launch_bounds__(LW * 64) void lin_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, int K,
+                                                      float* __restrict__ sink) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nb = K / QK;
+    const long RB = (long)nb * 18, AB = (long)nb * 36;
+    const uint8_t* Bw = B + (long)blockIdx.x * BN * RB;
+    const uint8_t* Aw = A + (long)blockIdx.y * NT * AB;
+    const int WI = MODE == 2 ? 0 : (int)((BN * RB) / 1024);   // 1-KB weight pieces (RB * BN % 1024 == 0 here)
+    const int AI = MODE == 1 ? 0 : (int)((NT * AB) / 1024);
+    const int cpr = (int)((RB + 1023) / 1024);               // chunks per row (ORDER 1)
+    int n = 0;
+    for (int i = wave; i < WI + AI; i += LW) {
+        const uint8_t* src;
+        if (i < WI) {
+            long off = (long)i * 1024;
+            if (ORDER == 1) {  // chunk-major: i -> (chunk c, row r), 1 KB of row r at c * 1 KB (clamped)
+                const int c = i / BN, r = i % BN;
+                off = (long)r * RB + std::min<long>((long)c * 1024, RB - 1024);
+                (void)cpr;
+            }
+            src = Bw + off + 16 * lane;
+            glds16<CP>(src, smem + ((long)i * 1024) % (144 * 1024));
+        } else {
+            src = Aw + (long)(i - WI) * 1024 + 16 * lane;
+            glds16<0>(src, smem + ((long)i * 1024) % (144 * 1024));
+        }
+        if (++n == 48) { vm_wait<16>(); n = 16; }
+    }
+    vm_wait<0>();
+    if (lane == 0 && K < 0) sink[blockIdx.x] = (float)smem[wave];
+}
+
 __global__ void empty_kernel(float* sink, int K) {
     if (K < 0) sink[0] = 1.0f;
 }
@@ -113,6 +153,23 @@ V mk(const char* name, int M, int N, int K, float* sink) {
                     set = true;
                 }
                 hipLaunchKernelGGL(k, dim3(N / BN, M / NT), dim3(LW * 64), lds, st, A, B, K, sink);
+            },
+            bytes};
+}
+
+template <int BN, int NT, int LW, int ORDER, int MODE, int CP>
+V mkl(const char* name, int M, int N, int K, float* sink) {
+    const double wb = (double)BN * K / 32 * 18, ab = (double)NT * K / 32 * 36;
+    const double bytes = MODE == 1 ? wb : MODE == 2 ? ab : wb + ab;
+    return {name,
+            [=](const uint8_t* A, const uint8_t* B, hipStream_t st) {
+                auto k = lin_kernel<BN, NT, LW, ORDER, MODE, CP>;
+                static bool set = false;
+                if (!set) {
+                    CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024));
+                    set = true;
+                }
+                hipLaunchKernelGGL(k, dim3(N / BN, M / NT), dim3(LW * 64), 144 * 1024, st, A, B, K, sink);
             },
             bytes};
 }
@@ -150,6 +207,18 @@ int main() {
         mk<16, 32, 16, 4, 2, 6, 0, 2>("B sb16 lw4 d2 acts", M, N, K, sink),
         // geometry C: 32 rows x 32 tokens, 128 WGs (half the CUs), 73.7 KB + 147 KB
         mk<32, 32, 16, 4, 2, 5, 0, 0>("C sb16 lw4 d2 (128 WGs)", M, N, K, sink),
+        // linear (address-order) ingest of the same bytes
+        mkl<32, 16, 8, 0, 1, 0>("A lin lw8 weights", M, N, K, sink),
+        mkl<32, 16, 8, 1, 1, 0>("A lin lw8 weights chunk-major", M, N, K, sink),
+        mkl<32, 16, 8, 0, 2, 0>("A lin lw8 acts", M, N, K, sink),
+        mkl<32, 16, 8, 0, 0, 0>("A lin lw8 both", M, N, K, sink),
+        mkl<32, 16, 8, 1, 0, 0>("A lin lw8 both chunk-major", M, N, K, sink),
+        mkl<32, 16, 4, 0, 0, 0>("A lin lw4 both", M, N, K, sink),
+        mkl<32, 16, 16, 0, 0, 0>("A lin lw16 both", M, N, K, sink),
+        mkl<32, 16, 8, 0, 0, 2>("A lin lw8 both nt", M, N, K, sink),
+        mkl<16, 32, 8, 0, 1, 0>("B lin lw8 weights", M, N, K, sink),
+        mkl<16, 32, 8, 0, 0, 0>("B lin lw8 both", M, N, K, sink),
+        mkl<16, 32, 8, 1, 0, 0>("B lin lw8 both chunk-major", M, N, K, sink),
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
