@@ -9,6 +9,11 @@
 //  * M  > 32: 32 rows x 32 tokens; 8 waves splitting K while that grid has <= 256 workgroups, else
 //    4 (two workgroups per CU under the kernel's register cap; mmq_probe_p4.txt, mmq_probe_mid.txt,
 //    mmq_probe_lb.txt: M=64 10.1 us, M=128 15.2 us, M=512 47 us with the MFMA-assisted epilogue)
+//  * round 4, measured and not adopted: the whole K of a 32 x 16 tile resident in LDS with every
+//    operand byte requested at entry and a barrier per 32-block phase (tools/archive/
+//    mmqr_resident_experiment.hpp; profiles/r04_tuning/ab_mmqr.txt: M = 32 6.91 -> 8.35 us, M = 24
+//    6.72 -> 8.20, N = 11008 14.7 -> 21.3; parity green) — with everything in flight no phase completes
+//    until most bytes have landed, so the compute no longer overlaps the ingest.
 #include "qg_mmq_kernel.hpp"
 
 namespace qg {

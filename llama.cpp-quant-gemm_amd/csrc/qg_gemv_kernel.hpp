@@ -227,10 +227,16 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // bit 32 — output stores as agent-scope atomic exchanges (executed at the memory side: no dirty L2 lines).
 // The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
 // minimal argument list.
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL>
+// TPW (tiles per workgroup, loop-free form only): the workgroup computes TPW consecutive row tiles of
+// one product — the activations are staged and their records read ONCE for all of them, and every
+// tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
+// outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
+// thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL, int TPW = 1>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
                                           int32_t* __restrict__ sumi_out, int tile_in = -1) {
+    static_assert(TPW == 1 || (ONEU && (ABL & ~32) == 0), "several tiles per workgroup: loop-free form only");
     using G = gemv_geom<F, BPL>;
     QG_STAMP(t0);
     QG_CLK(c0);
@@ -254,12 +260,19 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     // the linear order (N=32000: 12.55 us linear, 13.28 remapped).
     // (a grouped launch passes the workgroup's tile within its item, tile_in >= 0)
     const int tile = tile_in >= 0 ? tile_in : gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int row = tile * RPB + (tid >> 6) * RPW + lane / LPR;
-    const bool row_ok = row < N;
-
-    const uint8_t* wrow = B + (long)(row_ok ? row : 0) * ((long)U * G::UB);
-    auto load_unit = [&](uint32_t (&dst)[G::UDW], int u) {
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(wrow + (long)((row_ok && u < U) ? u : 0) * G::UB);
+    int rows[TPW];
+    bool rows_ok[TPW];
+    const uint8_t* wrows[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        rows[t] = (tile * TPW + t) * RPB + (tid >> 6) * RPW + lane / LPR;
+        rows_ok[t] = rows[t] < N;
+        wrows[t] = B + (long)(rows_ok[t] ? rows[t] : 0) * ((long)U * G::UB);
+    }
+    const int row = rows[0];
+    const bool row_ok = rows_ok[0];
+    auto load_unit = [&](uint32_t (&dst)[G::UDW], int u, int t = 0) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(wrows[t] + (long)((rows_ok[t] && u < U) ? u : 0) * G::UB);
         if constexpr (NT) {
 #pragma unroll
             for (int v = 0; v + 4 <= G::UDW; v += 4) {
@@ -278,12 +291,18 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     // record of activation block blk = m * nb + b: unit (m * U + b / BPL) = blk / BPL, slot b % BPL
     auto rec_of = [&](int blk) { return (blk / BPL) * G::REC_DW + (blk % BPL) * 12; };
     uint32_t cur[G::UDW];
+    uint32_t more[TPW > 1 ? TPW - 1 : 1][G::UDW];  // tiles 1.. of the workgroup (TPW > 1)
+    auto load_first = [&]() {
+        load_unit(cur, lir);
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) load_unit(more[t - 1], lir, t);
+    };
 
     // 1) activation block loads of this thread (one thread per block), the first before the
     //    weight stream; 2) the lane's first weight unit; 3) LDS records
     const int totb = M * nb;
     if constexpr ((ABL & 1) != 0) {
-        load_unit(cur, lir);
+        load_first();
     } else if constexpr (AIN == AIN_Q8_1) {
         uint32_t ab[9];
         auto load_ablk = [&](int g) {
@@ -292,7 +311,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
             for (int i = 0; i < 9; ++i) ab[i] = p[i];
         };
         if (tid < totb) load_ablk(tid);
-        load_unit(cur, lir);
+        load_first();
         for (int g = tid; g < totb; g += WGS) {
             if (g != tid) load_ablk(g);
             make_act_record<F>(ab, lds + rec_of(g));
@@ -301,7 +320,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
         const uint8_t* X = reinterpret_cast<const uint8_t*>(A);
         float xv[32];
         if (tid < totb) load_act_block<AIN>(X, tid, xv);
-        load_unit(cur, lir);
+        load_first();
         for (int g = tid; g < totb; g += WGS) {
             if (g != tid) load_act_block<AIN>(X, g, xv);
             uint32_t w[9];
@@ -319,8 +338,8 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
 
     // one unit of this lane: activation records preloaded (PRE) or read per block
-    auto do_unit = [&](int u) {
-        uint4 pre[PRE ? BPL : 1][PRE ? MT : 1][3];
+    uint4 pre[PRE ? BPL : 1][PRE ? MT : 1][3];
+    auto read_pre = [&](int u) {
         if constexpr (PRE) {
 #pragma unroll
             for (int bi = 0; bi < BPL; ++bi)
@@ -335,6 +354,8 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
+    };
+    auto dot_unit = [&](const uint32_t (&cur)[G::UDW], int u, int row, bool row_ok) {
         static_for<BPL>([&](auto BI) {
             constexpr int bi = decltype(BI)::value;
 #pragma unroll
@@ -366,7 +387,15 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
             }
         });
     };
+    auto do_unit = [&](int u) {
+        read_pre(u);
+        dot_unit(cur, u, row, row_ok);
+    };
     const int iters = (U + LPR - 1) / LPR;
+    if constexpr (TPW > 1) {
+        // tiles 1.. after tile 0 (below): the records read once, each tile its own sum and store
+        static_assert(!SUMI || TPW == 1, "parity hook: one tile per workgroup");
+    }
     if constexpr (ONEU) {
         if (lir < U) do_unit(lir);
     } else {
@@ -408,17 +437,36 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
                 }
         }
     }
+    if constexpr (TPW > 1 && !SUMI) {
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
+            if (lir < U) dot_unit(more[t - 1], lir, rows[t], rows_ok[t]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<LPR>(acc[m]);
+            if (rows_ok[t] && lir == LPR - 1) {
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    if (m < M) {
+                        if constexpr ((ABL & 32) != 0)
+                            (void)__hip_atomic_exchange(C + m * ldc_m + rows[t] * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else C[m * ldc_m + rows[t] * ldc_n] = acc[m];
+                    }
+            }
+        }
+    }
     QG_STAMP(t2);
     QG_CLK(c2);
     QG_STAMP_STORE(t0, tb, t1, tc, t2, c0, c2);
 }
 
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
-          bool ONEU = false, int ABL = 0>
+          bool ONEU = false, int ABL = 0, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    long sA, long sB, int M, int N, int K, float* __restrict__ C,
                                                    long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
-    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, ONEU, ABL>(A, B, sA, sB, M, N, K, C, sC, ldc_m, ldc_n, sumi_out);
+    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, ONEU, ABL, TPW>(A, B, sA, sB, M, N, K, C, sC, ldc_m, ldc_n, sumi_out);
 }
 
 // M = 2..8, one product: (A, B, M, N, K, out, ldc_m, ldc_n) with 32-bit output strides = 10 dwords
@@ -458,15 +506,37 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 // tile prefix table (a lane-parallel vector load + ballot, or 64 scalar compares): 1.72 / 2.10 us per
 // GEMV in a group of 64 vs 1.44 for the strided batch (the lookup sat in front of every workgroup's
 // weight stream).
-template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU>
+// Uniform groups (grp.tpi > 0: every item has tpi tiles, count % 8 == 0) run on a 1-D grid with an
+// item-per-XCD order: workgroup L is dispatched to XCD L % 8, and XCD x runs items x, x + 8, ... one
+// after the other, each item's tiles in order over its 32 CUs — so a CU sees 1/8 of the items, their
+// descriptors stay in its scalar cache (a first-touch descriptor load sits in front of every
+// workgroup's weight stream otherwise), and an item's activations and output lines stay in one XCD's L2.
+// (Mixed groups keep the 2-D grid: blockIdx.y = item, blockIdx.x its tile, XCD-aware within the item.)
+#ifndef QG_GEMVG_XCD
+// item-per-XCD order for uniform groups (A/B knob; off: profiles/r04_tuning — 64 GEMVs per grouped
+// launch 1.59 -> 1.64 us per GEMV with it)
+#define QG_GEMVG_XCD 0
+#endif
+#ifndef QG_GEMV_TPW
+#define QG_GEMV_TPW 2  // row tiles per workgroup of the batched / grouped loop-free launches (gemv_body)
+#endif
+template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
-    constexpr int RPB = (WGS / 64) * (64 / LPR);
-    const GemvItemDesc d = grp.it[blockIdx.y];
-    // the single launch's XCD-aware tile order (gemv_body) within the item: with grid.x a multiple of 8
-    // the workgroup's XCD is blockIdx.x % 8, so each XCD takes a contiguous range of the item's tiles
-    const int tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    constexpr int RPB = (WGS / 64) * (64 / LPR) * TPW;  // rows per workgroup
+    int item, tile;
+    if (grp.tpi > 0) {
+        const int L = blockIdx.x, j = L >> 3;
+        item = 8 * (j / grp.tpi) + (L & 7);
+        tile = j - (j / grp.tpi) * grp.tpi;
+    } else {
+        item = blockIdx.y;
+        // the single launch's XCD-aware tile order (gemv_body) within the item: with grid.x a multiple
+        // of 8 the workgroup's XCD is blockIdx.x % 8, so each XCD takes a contiguous range of its tiles
+        tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    }
+    const GemvItemDesc d = grp.it[item];
     if (tile * RPB >= d.N) return;  // past this item's rows (uniform)
-    gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, 0>(
+    gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, 0, TPW>(
         reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K, d.C, 0,
         d.ldc, 1, nullptr, tile);
 }
@@ -509,16 +579,25 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     }
     if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
         if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
-            const GemvGroup& grp = *static_cast<const GemvGroup*>(g.group);
-            int tiles = 0;
-            for (int i = 0; i < grp.count; ++i) tiles = std::max(tiles, (grp.it[i].N + RPB - 1) / RPB);
-            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true> : gemvg_kernel<F, MT, BPL, LPR, WGS, PRE && (MT <= 2), false>;
+            GemvGroup grp = *static_cast<const GemvGroup*>(g.group);
+            const int rpw = one ? RPB * QG_GEMV_TPW : RPB;  // rows per workgroup
+            int tiles = 0, tmin = INT32_MAX;
+            for (int i = 0; i < grp.count; ++i) {
+                const int t = (grp.it[i].N + rpw - 1) / rpw;
+                tiles = std::max(tiles, t);
+                tmin = std::min(tmin, t);
+            }
+            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true, QG_GEMV_TPW>
+                          : gemvg_kernel<F, MT, BPL, LPR, WGS, PRE && (MT <= 2), false>;
             if (lds > 64 * 1024) {
                 hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
             }
             if (tiles == 0 || grp.count == 0) return hipSuccess;
-            hipLaunchKernelGGL(kg, dim3(tiles, grp.count), dim3(WGS), lds, st, grp);
+            const bool uniform = QG_GEMVG_XCD && tiles == tmin && grp.count % 8 == 0 && (long)tiles * grp.count <= INT32_MAX;
+            grp.tpi = uniform ? tiles : 0;
+            const dim3 grid = uniform ? dim3(tiles * grp.count) : dim3(tiles, grp.count);
+            hipLaunchKernelGGL(kg, grid, dim3(WGS), lds, st, grp);
             return hipGetLastError();
         }
     }
@@ -545,14 +624,19 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                            (int)g.ldc_m, (int)g.ldc_n);
         return hipGetLastError();
     }
-    // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4)
-    auto kfn = one ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
-                   : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE && (MT <= 2), false>;
+    // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4); a strided
+    // batch of loop-free GEMVs takes QG_GEMV_TPW row tiles per workgroup (same per-row arithmetic)
+    constexpr bool tpw_ok = !SUMI && !NT && QG_GEMV_TPW > 1;
+    const bool multi = tpw_ok && one && g.batch > 1;
+    auto kfn = multi ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true, 0, tpw_ok ? QG_GEMV_TPW : 1>
+             : one   ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
+                     : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE && (MT <= 2), false>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kfn, dim3(grid, g.batch), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.sA,
+    const int gx = multi ? (g.N + RPB * QG_GEMV_TPW - 1) / (RPB * QG_GEMV_TPW) : grid;
+    hipLaunchKernelGGL(kfn, dim3(gx, g.batch), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.sA,
                        g.sB, g.M, g.N, g.K, g.C, g.sC, g.ldc_m, g.ldc_n, g.sumi);
     return hipGetLastError();
 }

@@ -41,7 +41,9 @@ struct GemvItemDesc {  // 32 B: one s_load_dwordx8 in the kernel
     int N, ldc;
 };
 struct GemvGroup {
-    int count, M, K, pad;
+    // tpi > 0: every item has tpi row tiles and count % 8 == 0, the grid is 1-D (count * tpi) and
+    // workgroup L runs item 8 (L / 8 / tpi) + L % 8, tile (L / 8) % tpi (qg_gemv_kernel.hpp, gemvg_kernel)
+    int count, M, K, tpi;
     GemvItemDesc it[GEMV_GROUP_MAX];
 };
 

@@ -46,6 +46,22 @@ def test_grouped_qkv_bit_identical(O, qg, t, m):
         close_to_oracle(O, got, aqs[i], bqs[i], t)
 
 
+@pytest.mark.parametrize("count,n,m,k,t", [(8, 4096, 1, 4096, 2), (16, 1000, 2, 2048, 6), (24, 300, 1, 1024, 3),
+                                           (64, 4096, 1, 4096, 2)])
+def test_grouped_uniform_item_per_xcd_order(O, qg, count, n, m, k, t):
+    """Uniform groups (same N for every item, count % 8 == 0) take the 1-D item-per-XCD grid; per-item
+    activations: every item's output still equals its single launch bit for bit."""
+    rng = np.random.default_rng(count * 31 + n)
+    items = [random_blocks(rng, m, n, k, t) for _ in range(min(count, 8))]
+    a_d = [dev(items[i % len(items)][0]) for i in range(count)]
+    b_d = [dev(items[i % len(items)][1]) for i in range(count)]
+    outs = qg.gemm_w4a8_grouped(a_d, b_d, [n] * count, m, k, t)
+    for i in range(count):
+        single = host(qg.gemm_w4a8(a_d[i], b_d[i], m, n, k, t))
+        assert np.array_equal(host(outs[i]).view(np.uint32), single.view(np.uint32)), f"item {i}"
+    close_to_oracle(O, host(outs[0]), items[0][0], items[0][1], t)
+
+
 def test_grouped_per_item_activations_strided_outputs(O, qg):
     import torch
     rng = np.random.default_rng(7)

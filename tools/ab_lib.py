@@ -40,12 +40,20 @@ def main() -> None:
     ap.add_argument("--libs", nargs="+", required=True)
     ap.add_argument("--shapes", default="1x4096x4096:2,32x4096x4096:2")
     ap.add_argument("--algo", type=int, default=0)
+    ap.add_argument("--algos", default="", help="one library, several algo ids (e.g. 0,5): variants = algos; "
+                    "outputs compared by max relative difference instead of bit for bit")
     ap.add_argument("--G", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--w16", action="store_true", help="time qg_gemm_w4a16 (fp32 activations, Q4_0 weights)")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
+    algos = [a.algo] * len(libs)
+    names = list(a.libs)
+    if a.algos:
+        algos = [int(x) for x in a.algos.split(",")]
+        libs = [libs[0]] * len(algos)
+        names = [f"{os.path.basename(a.libs[0])} algo {x}" for x in algos]
     dev = torch.device("cuda", 0)
     for spec in a.shapes.split(","):
         dims, wt = spec.split(":")
@@ -71,7 +79,7 @@ def main() -> None:
                                                   P(outs[li, j].data_ptr()), M, N, K, P(wss[li].data_ptr()), WSB, st)
                     else:
                         rc = lib.qg_gemm_w4a8_ex(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
-                                                 P(outs[li, j].data_ptr()), M, N, K, wt, a.algo, st)
+                                                 P(outs[li, j].data_ptr()), M, N, K, wt, algos[li], st)
                     assert rc == 0, rc
             side = torch.cuda.Stream()
             with torch.cuda.stream(side):
@@ -83,7 +91,8 @@ def main() -> None:
             graphs.append(g)
         for li in range(1, len(libs)):
             if not torch.equal(outs[0], outs[li]):
-                print(f"  !! {a.libs[li]} differs from {a.libs[0]} at {spec}")
+                rel = ((outs[li] - outs[0]).abs().max() / outs[0].abs().max()).item()
+                print(f"  {'!!' if not a.algos else '..'} {names[li]} differs from {names[0]} at {spec} (max rel {rel:.2e})")
         times = [[] for _ in libs]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(a.rounds):
@@ -99,7 +108,7 @@ def main() -> None:
         bb = qg.BLOCK_BYTES[wt]
         nbytes = N * nb * bb + M * K * (4 if a.w16 else 36 / 32) + M * N * 4
         print(f"M={M} N={N} K={K} wtype={wt} ({nbytes} B/launch, {R} copies)")
-        for li, p in enumerate(a.libs):
+        for li, p in enumerate(names):
             med = statistics.median(times[li])
             print(f"  {os.path.basename(p):28s} {med:7.3f} us  (min {min(times[li]):.3f} max {max(times[li]):.3f})"
                   f"  {nbytes / med / 1e3:7.1f} GB/s  frac {nbytes / med / 8e6:.3f}")
