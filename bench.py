@@ -405,7 +405,17 @@ def native_leg(wc, aq, M: int, G: int, n_total: int, K: int, wt: int, world: int
     import ctypes
 
     from quant_gemm.sharded import NcclComm, shard_lib
-    lib = shard_lib()
+    # every rank agrees before the collective communicator init (a rank that cannot load the library
+    # must not leave the others waiting inside ncclCommInitRank)
+    try:
+        lib = shard_lib()
+        ok = 1
+    except Exception:  # noqa: BLE001
+        lib, ok = None, 0
+    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        raise RuntimeError("libqg_shard.so did not load on every rank")
     comm = NcclComm()
     P = ctypes.c_void_p
     rows = rows_per_rank(n_total, world)
