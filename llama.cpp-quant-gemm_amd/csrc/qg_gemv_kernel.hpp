@@ -517,8 +517,15 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 // launch 1.59 -> 1.64 us per GEMV with it)
 #define QG_GEMVG_XCD 0
 #endif
+// row tiles per workgroup of the loop-free launches (gemv_body TPW): grouped (QG_GEMVG_TPW) and strided
+// batch (QG_GEMV_TPW). profiles/r04_tuning/r04d_bench_tpw*.json, 64 GEMVs (M = 1, N = K = 4096) per
+// launch: grouped 1.606 -> 1.529 us per GEMV with 2 (one descriptor load and one activation staging per
+// two tiles), strided batch 1.450 -> 1.452 (no descriptor to amortise: kept at 1)
 #ifndef QG_GEMV_TPW
-#define QG_GEMV_TPW 2  // row tiles per workgroup of the batched / grouped loop-free launches (gemv_body)
+#define QG_GEMV_TPW 1
+#endif
+#ifndef QG_GEMVG_TPW
+#define QG_GEMVG_TPW 2
 #endif
 template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
@@ -580,14 +587,14 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
         if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
             GemvGroup grp = *static_cast<const GemvGroup*>(g.group);
-            const int rpw = one ? RPB * QG_GEMV_TPW : RPB;  // rows per workgroup
+            const int rpw = one ? RPB * QG_GEMVG_TPW : RPB;  // rows per workgroup
             int tiles = 0, tmin = INT32_MAX;
             for (int i = 0; i < grp.count; ++i) {
                 const int t = (grp.it[i].N + rpw - 1) / rpw;
                 tiles = std::max(tiles, t);
                 tmin = std::min(tmin, t);
             }
-            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true, QG_GEMV_TPW>
+            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true, QG_GEMVG_TPW>
                           : gemvg_kernel<F, MT, BPL, LPR, WGS, PRE && (MT <= 2), false>;
             if (lds > 64 * 1024) {
                 hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
