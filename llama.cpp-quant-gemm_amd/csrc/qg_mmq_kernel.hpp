@@ -106,7 +106,10 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // profiles/r01_tuning/mmq_timeline_r01e.txt). Each stage's partial tile goes to its own LDS slot and
 // the slots are summed in stage order at the end: bit-identical whichever wave took which stage.
 // A tuning option (QG_MMQ_DYN, qg_gemm_mfma.hip): measured slower, off in the product.
-enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4 };
+// MMQ_EARLY — the refill of a consumed stage buffer (the DMA of the wave's stage k + NB) is issued as
+// soon as the buffer's operand reads have returned, before the stage's MFMAs and epilogue, instead of
+// after them: the next DMA's latency starts one compute phase earlier (round 4).
+enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4, MMQ_EARLY = 8 };
 constexpr int MMQ_ZB = 1024;  // bytes of the per-wave zero region (covers every scale offset)
 
 template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4, int OPT = 0> struct mmq_geom {
@@ -372,7 +375,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
             for (int t = 0; t < TT; ++t) c2[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
     }
     auto h4 = [](unsigned long v) { return __builtin_bit_cast(f16x4, v); };
-    auto compute4_e2 = [&](uint8_t* buf, int h, int sh, auto SUB) {
+    auto compute4_e2 = [&](uint8_t* buf, int h, int sh, auto SUB, auto&& after_reads) {
         constexpr int b0 = 4 * decltype(SUB)::value;
         (void)h;
         long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
@@ -398,6 +401,8 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
                 adb[b][t] = *reinterpret_cast<const uint32_t*>(as + (b0 + b) * Q8_1_BYTES);  // f16 d_a | f16 s_a << 16
             }
         });
+        __builtin_amdgcn_sched_barrier(0);
+        after_reads();  // MMQ_EARLY: the buffer's refill (its LDS reads are waited for first: WAR on the buffer)
         __builtin_amdgcn_sched_barrier(0);
         f32x4v dd[MMQ_SB][G::RT][TT];
         v4i cc[MMQ_SB][G::RT][TT];
@@ -533,9 +538,12 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    auto compute = [&](uint8_t* buf, int h, int sh) {
+    auto compute = [&](uint8_t* buf, int h, int sh, auto&& after_reads) {
         if constexpr (EPI2 && ABL == 0)
-            static_for<SB / 4>([&](auto SUB) { compute4_e2(buf, h, sh, SUB); });
+            static_for<SB / 4>([&](auto SUB) {
+                if constexpr (decltype(SUB)::value == SB / 4 - 1) compute4_e2(buf, h, sh, SUB, after_reads);
+                else compute4_e2(buf, h, sh, SUB, [] {});
+            });
         else
             static_for<SB / 4>([&](auto SUB) { compute4(buf, h, sh, SUB); });
     };
@@ -595,7 +603,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
 #pragma unroll
                     for (int t = 0; t < TT; ++t) c2[i][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
             }
-            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(bA, ha, G::shift(ha));
+            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(bA, ha, G::shift(ha), [] {});
             if constexpr (!SUMI) {
                 if constexpr (EPI2 && HAS_S) {
                     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // margin: the stage's compensation MFMAs
@@ -648,11 +656,16 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     #ifdef QG_MMQ_STAMPS
             if (k == 0) MMQ_STAMP(1);
     #endif
-            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) compute(cur, h, G::shift(h));
+            constexpr bool early = (OPT & MMQ_EARLY) != 0 && EPI2 && ABL == 0;
+            if constexpr (ABL != 1 && ABL != 3 && ABL != 4) {
+                if constexpr (early) compute(cur, h, G::shift(h), [&] { if (k + NB < nst) issue(stage(k + NB), cur); });
+                else compute(cur, h, G::shift(h), [] {});
+            }
     #ifdef QG_MMQ_STAMPS
             if (k == 0) MMQ_STAMP(2);
     #endif
-            if (k + NB < nst) issue(stage(k + NB), cur);  // refill the buffer just consumed
+            if constexpr (!early)
+                if (k + NB < nst) issue(stage(k + NB), cur);  // refill the buffer just consumed
         }
         MMQ_STAMP(3);
     
