@@ -45,9 +45,13 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #ifndef QG_MMQ_EARLY
 #define QG_MMQ_EARLY 1
 #endif
+// Raw weight-fragment reads in one batch per stage (MMQ_RAW): A/B knob
+#ifndef QG_MMQ_RAW
+#define QG_MMQ_RAW 0
+#endif
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;
-    constexpr int E = QG_MMQ_EARLY ? MMQ_EARLY : 0;
+    constexpr int E = (QG_MMQ_EARLY ? MMQ_EARLY : 0) | (QG_MMQ_RAW ? MMQ_RAW : 0);
     if constexpr (QG_MMQ_DYN && BN == 32 && TT == 1 && W == 8) {
         if (mmq_geom<F, BN, TT, W, P16, 2, 4, MMQ_DYN>::dyn_lds(g.K / QK / 4) <= 160 * 1024) {
             if (g.sumi) return mmq_launch<F, BN, TT, W, true, P16, 2, 0, false, 4, 1, true, MMQ_DYN, S>(g, st);

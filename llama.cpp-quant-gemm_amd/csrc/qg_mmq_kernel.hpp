@@ -109,7 +109,10 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 // MMQ_EARLY — the refill of a consumed stage buffer (the DMA of the wave's stage k + NB) is issued as
 // soon as the buffer's operand reads have returned, before the stage's MFMAs and epilogue, instead of
 // after them: the next DMA's latency starts one compute phase earlier (round 4).
-enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4, MMQ_EARLY = 8 };
+// MMQ_RAW — the EPI2 stage's weight fragments are read as raw dwords first (every LDS read of the stage
+// in one batch, one lgkmcnt wait) and realigned / split into nibbles afterwards; without it hipcc
+// interleaves the realignment with the reads and waits for the LDS twice per stage (round 4).
+enum : int { MMQ_CONTIG = 1, MMQ_ZL = 2, MMQ_DYN = 4, MMQ_EARLY = 8, MMQ_RAW = 16 };
 constexpr int MMQ_ZB = 1024;  // bytes of the per-wave zero region (covers every scale offset)
 
 template <int F, int BN, int TT, int W, bool P16 = false, int NB = 2, int SB = 4, int OPT = 0> struct mmq_geom {
@@ -381,13 +384,34 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
         long afrag[MMQ_SB][G::RT], bfrag[MMQ_SB][TT];
         uint32_t wdb[MMQ_SB][G::RT], wmb[MMQ_SB][G::RT], adb[MMQ_SB][TT];
         const bool q0 = q == 0;
+        constexpr bool RAW = (OPT & MMQ_RAW) != 0;
+        // raw weight dwords (MMQ_RAW): [0] / [1] the qs dword(s) at o + QS + 4q (two when not 4-B aligned),
+        // [2] / [3] the same 16 bytes on (Q8_0's high dword), [4] / [5] the qh dword (Q5_x)
+        uint32_t wraw[RAW ? MMQ_SB : 1][RAW ? G::RT : 1][6];
         static_for<MMQ_SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
             constexpr int o = (b0 + b) * T::BB;
 #pragma unroll
             for (int i = 0; i < G::RT; ++i) {
                 const uint8_t* wr = buf + (16 * i + r16) * G::RIMG + sh;
-                afrag[b][i] = wfrag(wr, ic<o>{});
+                if constexpr (RAW) {
+                    constexpr int qo = o + T::QS, qa = qo % 4;
+                    const uint32_t* p = reinterpret_cast<const uint32_t*>(wr + 4 * q + (qo & ~3));
+                    wraw[b][i][0] = p[0];
+                    if constexpr (qa != 0) wraw[b][i][1] = p[1];
+                    if constexpr (T::Q8) {
+                        wraw[b][i][2] = p[4];
+                        if constexpr (qa != 0) wraw[b][i][3] = p[5];
+                    }
+                    if constexpr (T::QH >= 0) {
+                        constexpr int ho = o + T::QH;
+                        const uint32_t* ph = reinterpret_cast<const uint32_t*>(wr + (ho & ~3));
+                        wraw[b][i][4] = ph[0];
+                        if constexpr (ho % 4 != 0) wraw[b][i][5] = ph[1];
+                    }
+                } else {
+                    afrag[b][i] = wfrag(wr, ic<o>{});
+                }
                 const uint8_t* ws = ZL ? (q0 ? wr : zb) : wr;  // ZL: lanes q > 0 read zeros
                 wdb[b][i] = u16(ws + o);
                 if constexpr (HAS_M) wmb[b][i] = u16(ws + o + T::MOFF);
@@ -404,6 +428,38 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
         __builtin_amdgcn_sched_barrier(0);
         after_reads();  // MMQ_EARLY: the buffer's refill (its LDS reads are waited for first: WAR on the buffer)
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (RAW) {  // realign + nibble split (wfrag's arithmetic) now that every read has returned
+            static_for<MMQ_SB>([&](auto BI) {
+                constexpr int b = decltype(BI)::value;
+                constexpr int o = (b0 + b) * T::BB;
+                constexpr int qa = (o + T::QS) % 4;
+#pragma unroll
+                for (int i = 0; i < G::RT; ++i) {
+                    auto al = [&](int k) {
+                        if constexpr (qa == 0) return wraw[b][i][k];
+                        else return __builtin_amdgcn_alignbyte(wraw[b][i][k + 1], wraw[b][i][k], qa);
+                    };
+                    uint32_t lo, hi;
+                    if constexpr (T::Q8) {
+                        lo = al(0);
+                        hi = al(2);
+                    } else {
+                        const uint32_t v = al(0);
+                        lo = v & 0x0F0F0F0Fu;
+                        hi = (v >> 4) & 0x0F0F0F0Fu;
+                    }
+                    if constexpr (T::QH >= 0) {
+                        constexpr int ha = (o + T::QH) % 4;
+                        uint32_t qh;
+                        if constexpr (ha == 0) qh = wraw[b][i][4];
+                        else qh = __builtin_amdgcn_alignbyte(wraw[b][i][5], wraw[b][i][4], ha);
+                        lo |= spread4_bit4((qh >> (4 * q)) & 0xFu);
+                        hi |= spread4_bit4((qh >> (16 + 4 * q)) & 0xFu);
+                    }
+                    afrag[b][i] = (long)(((unsigned long)hi << 32) | lo);
+                }
+            });
+        }
         f32x4v dd[MMQ_SB][G::RT][TT];
         v4i cc[MMQ_SB][G::RT][TT];
         const f32x4v z4 = {0.f, 0.f, 0.f, 0.f};

@@ -15,5 +15,5 @@ tail -2 $OUT/grouped.txt
 timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err
 python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['roofline']['us_per_launch'],d['batched'],d['grouped'])"
 cp tools/variants/libqg_mmqr.so llama.cpp-quant-gemm_amd/quant_gemm/libqg_hip.so
-timeout -k 10 400 python -u -m pytest tests/test_gpu_00_baseline.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_boundary.py -x -q --timeout 120 --timeout-method thread > $OUT/mmqr_parity.txt 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_00_gpu_baseline.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_boundary.py -x -q --timeout 120 --timeout-method thread > $OUT/mmqr_parity.txt 2>&1
 tail -3 $OUT/mmqr_parity.txt

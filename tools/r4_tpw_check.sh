@@ -5,7 +5,7 @@
 set -e
 OUT=gpurun_out/r4d
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_parity.py tests/test_gpu_00_baseline.py tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.txt 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_parity.py tests/test_00_gpu_baseline.py tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.txt 2>&1
 tail -2 $OUT/tests.txt
 timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench_tpw2.json 2> $OUT/bench_tpw2.err
 python -c "import json;d=json.load(open('$OUT/bench_tpw2.json'));print('tpw2',d['roofline']['us_per_launch'],d['batched'],d['grouped'],[(s['N'],s['form'],s.get('us_per_gemv',s.get('us_per_launch'))) for s in d['side_configs']])"
