@@ -41,9 +41,13 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #ifndef QG_MMQ_DYN
 #define QG_MMQ_DYN 0
 #endif
-// Early refill of consumed stage buffers (MMQ_EARLY, qg_mmq_kernel.hpp): A/B knob
+// Early refill of consumed stage buffers (MMQ_EARLY, qg_mmq_kernel.hpp): A/B knob, off — measured
+// slower at the prefill sizes that matter (profiles/r04_tuning/ab_early.txt: M = 32 6.90 -> 7.14 us,
+// M = 16 5.47 -> 5.54, N = 11008 14.55 -> 14.90, M = 64 9.69 -> 9.92; M = 8 -0.1 us, M = 512 -0.45);
+// the refill must wait for the stage's LDS reads (lgkmcnt(0)), which takes the overlap away. Its first
+// form, without that wait, was non-deterministic (profiles/r04_tuning/r04g_gpu_suite_fail_early_unwaited.txt).
 #ifndef QG_MMQ_EARLY
-#define QG_MMQ_EARLY 1
+#define QG_MMQ_EARLY 0
 #endif
 // Raw weight-fragment reads in one batch per stage (MMQ_RAW): A/B knob
 #ifndef QG_MMQ_RAW

@@ -426,7 +426,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
             }
         });
         __builtin_amdgcn_sched_barrier(0);
-        after_reads();  // MMQ_EARLY: the buffer's refill (its LDS reads are waited for first: WAR on the buffer)
+        after_reads();  // MMQ_EARLY: the buffer's refill (it waits for the LDS reads itself: WAR on the buffer)
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (RAW) {  // realign + nibble split (wfrag's arithmetic) now that every read has returned
             static_for<MMQ_SB>([&](auto BI) {
@@ -714,7 +714,16 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     #endif
             constexpr bool early = (OPT & MMQ_EARLY) != 0 && EPI2 && ABL == 0;
             if constexpr (ABL != 1 && ABL != 3 && ABL != 4) {
-                if constexpr (early) compute(cur, h, G::shift(h), [&] { if (k + NB < nst) issue(stage(k + NB), cur); });
+                // the refill overwrites `cur`: every LDS read of it must have returned first (hipcc does
+                // not order a global_load_lds after earlier ds_reads of the same bytes — round 4 found the
+                // unwaited form non-deterministic on the GPU, tests/test_gpu_fused.py)
+                if constexpr (early)
+                    compute(cur, h, G::shift(h), [&] {
+                        if (k + NB < nst) {
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            issue(stage(k + NB), cur);
+                        }
+                    });
                 else compute(cur, h, G::shift(h), [] {});
             }
     #ifdef QG_MMQ_STAMPS
