@@ -14,6 +14,12 @@
 //    mmqr_resident_experiment.hpp; profiles/r04_tuning/ab_mmqr.txt: M = 32 6.91 -> 8.35 us, M = 24
 //    6.72 -> 8.20, N = 11008 14.7 -> 21.3; parity green) — with everything in flight no phase completes
 //    until most bytes have landed, so the compute no longer overlaps the ingest.
+//  * round 4, measured and not adopted: a chunked, workgroup-cooperative ingest (576-B row segments
+//    instead of 72 B, one barrier per 32-block chunk; tools/archive/mmqc_experiment.hpp,
+//    profiles/r04_tuning/ab_mmqc_v1.txt: M = 32 6.91 -> 8.54 us, N = 11008 14.7 -> 22.3). Its per-wave
+//    timeline (mmqc_probe_v1.txt) shows why: the coalesced chunks all land together ~2.8 us after entry
+//    (DMA + barriers alone 5.3 us per launch), and the lockstep compute then costs ~0.9-1.0 us per chunk
+//    (the LDS reads, 16-cycle MFMAs and epilogue of 8 waves serialise), 4 chunks after the data.
 #include "qg_mmq_kernel.hpp"
 
 namespace qg {
