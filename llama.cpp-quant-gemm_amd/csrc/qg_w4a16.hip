@@ -1142,6 +1142,203 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
     if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Round-4 small-M prefill without split-K (the split-K hand-off of w16s_kernel
+// — 8 KB partial slab per workgroup, counter, last-arriver sum — cost ~5 us and 9x the output in
+// writes at M = 32). A workgroup owns 16 RT weight rows x 16 tokens and ALL of K; its W waves take
+// the 2-block stages h = w, w + W, ... through wave-private LDS-DMA rings (NB slots, counted vmcnt,
+// no barrier in the main loop, as qg_mmq_kernel.hpp): per stage the RT x 16-row weight windows (48 B
+// each: the 36-B segment sits 0 / 4 / 8 / 12 B into a 16-B aligned window) and the 16 tokens' raw fp32
+// activations (256 B per token + 32 B pad: the ds_read_b128 fragment reads of a lane group hit distinct
+// banks). Each lane reads its token's k-slot (elements 4q.., 16+4q..) of a block as two ds_read_b128
+// and splits it in registers (w16_afrag2 / w16_afrag: nothing written back to LDS, so no LDS store ever
+// waits for the DMA), its weight row's qs dword q -> 8 exact bf16 of q - 8 (w16s_wfrag), NP chained
+// v_mfma_f32_16x16x32_bf16 per (block, row tile), acc += d_w * dot. The W partial tiles are summed in
+// fixed wave order through LDS at the end: deterministic, and the only global writes are the outputs.
+// 32 bits at byte offset (compile-time OFF) of an LDS row, from aligned dword reads
+template <int OFF> __device__ __forceinline__ uint32_t w16_lds32(const uint8_t* base) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (OFF & ~3));
+    if constexpr (OFF % 4 == 0) return p[0];
+    else return __builtin_amdgcn_alignbyte(p[1], p[0], OFF % 4);
+}
+
+template <int F, int RT, int W, int NP, int SB_ = 2> struct w16d_geom {
+    static constexpr int BB = wfmt<F>::BB;
+    static constexpr int SB = SB_;                         // blocks per stage
+    static constexpr int RSB = SB * BB;                    // 36 (Q4_0) / 68 (Q8_0) weight bytes per row
+    // a stage's row segment starts (h * RSB) % 16 bytes into its 16-B aligned window: at most
+    // SHMAX = 16 - gcd(RSB, 16); the window ends at the row's end for the last stage exactly when its
+    // shift is SHMAX, i.e. RSB % 16 is 0 or gcd(RSB, 16) (36, 68, 72, 136 B: yes) — no read past a row
+    static constexpr int G16 = (RSB & 15) == 0 ? 16 : (RSB & -RSB);
+    static constexpr int SHMAX = 16 - G16;
+    static constexpr int RIMG = RSB + SHMAX;
+    static constexpr int RP = RIMG / 16;
+    static constexpr int ROWS = 16 * RT;
+    static constexpr int WP = ROWS * RP;                   // weight pieces per stage
+    static constexpr int ATS = SB * 8 + 2;                 // pieces per token image (256 B + 32 B pad)
+    static constexpr int AP = 16 * ATS;
+    static constexpr int NI = (WP + AP + 63) / 64;         // DMA instructions per stage
+    static constexpr int SBYTES = NI * 1024;
+    static constexpr int AOFF = WP * 16;
+    static constexpr int NB = (160 * 1024) / (W * SBYTES) >= 3 ? 3 : 2;  // stage slots per wave
+    static constexpr int NACC = RT * 4;
+    static constexpr size_t LDS = (size_t)W * NB * SBYTES;
+    static_assert(LDS <= 160 * 1024 && (size_t)W * NACC * 64 * 4 <= LDS, "LDS per workgroup");
+    static_assert((NB - 1) * NI <= 63, "vmcnt range");
+    static_assert(RIMG % 16 == 0 && ((RSB & 15) == 0 || (RSB & 15) == G16), "windows end inside the row");
+};
+
+// ABL (tuning probes only; the product uses 0): 1 = DMA and waits without compute, 2 = compute without DMA.
+template <int F, int RT, int W, int NP, int SB = 2, int ABL = 0>
+__global__ __launch_bounds__(W * 64, 1) void w16d_kernel(const float* __restrict__ A, const uint8_t* __restrict__ B,
+                                                         float* __restrict__ C, int M, int N, int K, int ldc_m, int ldc_n) {
+    using G = w16d_geom<F, RT, W, NP, SB>;
+    using T = wfmt<F>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int n0 = blockIdx.x * G::ROWS, m0 = blockIdx.y * 16;
+    const int nst = K / (QK * G::SB);
+    const long RB = (long)(K / QK) * G::BB;
+    uint8_t* bufs = lds + wave * G::NB * G::SBYTES;
+
+    // per-lane DMA offsets of a stage (32-bit, relative to stage 0 of the tile's first row / token; rows
+    // / tokens past the edge re-read the last valid one, their results are dropped; pad pieces re-read
+    // the image's last data piece). Instructions wholly inside the weight or the activation images
+    // address from one wave-uniform 64-bit base (the saddr form: no per-lane 64-bit math per issue);
+    // only the one instruction that straddles both selects per lane.
+    const uint8_t* Bw = B + (long)n0 * RB;
+    const uint8_t* Aw = reinterpret_cast<const uint8_t*>(A + (long)m0 * K);
+    uint32_t off[G::NI];
+    bool isw[G::NI];
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        const int p = min(64 * i + lane, G::WP + G::AP - 1);
+        isw[i] = p < G::WP;
+        if (isw[i]) {
+            const int row = p / G::RP, j = p - row * G::RP;
+            off[i] = (uint32_t)((long)(min(n0 + row, N - 1) - n0) * RB + 16 * j);
+        } else {
+            const int a = p - G::WP, tok = a / G::ATS, j = min(a - tok * G::ATS, G::SB * 8 - 1);
+            off[i] = (uint32_t)((long)(min(m0 + tok, M - 1) - m0) * K * 4 + 16 * j);
+        }
+    }
+    // buffer resources over the tile's weight rows / token rows (raw byte buffers: a load past
+    // num_records returns zeros instead of faulting)
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Bw, (short)0, (int)min((long)(N - n0) * RB, 0x7FFFFFF0L), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)Aw, (short)0, (int)min((long)(M - m0) * K * 4, 0x7FFFFFF0L), 0x00020000);
+    auto issue = [&](int h, uint8_t* buf) {
+        if constexpr (ABL == 2) return;
+        const int dw = h * G::RSB - ((h * G::RSB) & 15), da = h * (G::SB * QK * 4);
+        static_for<G::NI>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            auto dst = (__attribute__((address_space(3))) void*)(buf + 1024 * i);
+            if constexpr (64 * i + 63 < G::WP) __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, dst, 16, (int)off[i], dw, 0, 0);
+            else if constexpr (64 * i >= G::WP) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, (int)off[i], da, 0, 0);
+            else w16_glds16((isw[i] ? Bw + dw : Aw + da) + off[i], buf + 1024 * i);
+        });
+    };
+
+    f32x4_t acc[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int mine = wave < nst ? (nst - 1 - wave) / W + 1 : 0;
+#pragma unroll
+    for (int k = 0; k < G::NB; ++k)
+        if (k < mine) issue(wave + k * W, bufs + k * G::SBYTES);
+    for (int k = 0; k < mine; ++k) {
+        const int h = wave + k * W;
+        uint8_t* buf = bufs + (k % G::NB) * G::SBYTES;
+        const int younger = ABL == 2 ? 0 : min(mine - 1 - k, G::NB - 1);
+        if (younger <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::NI) : "memory");
+        // operands of the stage's SB blocks: every LDS read first, then the splits / decodes, MFMAs, epilogue
+        const int sh = (h * G::RSB) & 15;
+        f32x4_t xa[G::SB][2];
+        uint32_t wv[G::SB][RT][2];
+        uint32_t wd[G::SB][RT];
+        static_for<G::SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+            const uint8_t* ar = buf + G::AOFF + r16 * (G::ATS * 16) + b * (QK * 4) + 16 * q;
+            xa[b][0] = *reinterpret_cast<const f32x4_t*>(ar);
+            xa[b][1] = *reinterpret_cast<const f32x4_t*>(ar + 64);
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const uint8_t* row = buf + (16 * i + r16) * G::RIMG + sh;
+                wv[b][i][0] = w16_lds32<b * G::BB + 2>(row + 4 * q);
+                if constexpr (T::Q8) wv[b][i][1] = w16_lds32<b * G::BB + 2 + 16>(row + 4 * q);
+                wd[b][i] = *reinterpret_cast<const uint16_t*>(row + b * G::BB);
+            }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ABL == 1) {
+            if (k + G::NB < mine) issue(h + G::NB * W, buf);
+            continue;
+        }
+        if (k + G::NB < mine) {  // every LDS read of this buffer has returned: refill it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(h + G::NB * W, buf);
+        }
+        f32x4_t c[G::SB][RT];
+        static_for<G::SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+            u32x4_t ap[NP];
+            if constexpr (NP == 2) {
+                w16_afrag2(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[0], ap[1]);
+            } else {
+                u32x4_t lo;
+                w16_afrag(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[0], ap[1], lo);
+                ap[NP - 1] = lo;
+            }
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const u32x4_t wf = T::Q8 ? w16s_wfrag_q8(wv[b][i][0], wv[b][i][1]) : w16s_wfrag(wv[b][i][0]);
+                c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0]), __builtin_bit_cast(bf16x8_t, wf),
+                                                                  f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                for (int pl = 1; pl < NP; ++pl)
+                    c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl]),
+                                                                      __builtin_bit_cast(bf16x8_t, wf), c[b][i], 0, 0, 0);
+            }
+        });
+        // MFMA results read by the VALU behind an explicit wait (8 states needed; qg_mmq_kernel.hpp)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<G::SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+                const float d = h2f(wd[b][i]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][e] = __builtin_fmaf(d, c[b][i][e], acc[i][e]);
+            }
+        });
+    }
+
+    // fixed-order sum of the W partial tiles (every DMA has landed: the last wait was vmcnt(0))
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[(wave * G::NACC + 4 * i + e) * 64 + lane] = acc[i][e];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G::NACC * 64; idx += W * 64) {
+        float v = red[idx];
+#pragma unroll
+        for (int ww = 1; ww < W; ++ww) v += red[ww * G::NACC * 64 + idx];
+        const int x = idx >> 6, ln = idx & 63;
+        const int e = x & 3, i = x >> 2;
+        const int n = n0 + 16 * i + (ln & 15);      // lane's column: weight row r16
+        const int m = m0 + 4 * (ln >> 4) + e;       // rows 4q + e: tokens
+        if (n < N && m < M) C[(long)m * ldc_m + (long)n * ldc_n] = v;
+    }
+}
+
 #ifndef QG_GEMV_SMALLK
 #define QG_GEMV_SMALLK 1
 #endif
@@ -1379,7 +1576,55 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
     return w16_sk_launch_np<F, RT, TT, KB, 3>(g, p, ws, st);
 }
 
+#ifndef QG_W16D
+#define QG_W16D 1  // the no-split-K small-M prefill (w16d_kernel) where w16d_ok holds
+#endif
+#ifndef QG_W16D_MAXK
+#define QG_W16D_MAXK 8192  // beyond, the split-K kernel is faster (K = 14336: 30.4 vs 29.4 us, ab_w16d_v2.txt)
+#endif
+// 8 < M <= 32 tokens, K % 256 == 0 (16-B aligned weight rows), 16-B aligned operands, 32-bit strides.
+// One dispatch round only (<= 256 workgroups): with more, each CU runs several workgroups in turn
+// (one fits at a time) and the split-K kernel is faster (M = 32, N = 11008: 29.6 vs 23.5 us,
+// profiles/r04_tuning/ab_w16d_v1.txt).
+inline bool w16d_ok(const GemmArgs& g) {
+    if (!(QG_W16D && g.M > 8 && g.M <= 32 && g.N >= 1 && g.K % 256 == 0 && ((uintptr_t)g.A & 15) == 0 &&
+          ((uintptr_t)g.B & 15) == 0 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX))
+        return false;
+    const long rows = (g.N + 15) / 16 * ((g.M + 15) / 16);  // 16-row tiles
+    return (rows <= 256 || (long)((g.N + 31) / 32) * ((g.M + 15) / 16) <= 256) && g.K <= QG_W16D_MAXK &&
+           (long)g.M * g.K * 4 < 0x7FFFFFF0L && (long)g.N * (g.K / QK) * wfmt<FMT_Q8_0>::BB < 0x7FFFFFF0L;  // buffer ranges
+}
+#ifndef QG_W16D_W
+#define QG_W16D_W 8  // waves per workgroup (tuning knob)
+#endif
+#ifndef QG_W16D_SB
+#define QG_W16D_SB 2  // blocks per stage (tuning knob; 4 needs QG_W16D_W 4 for the LDS)
+#endif
+#ifndef QG_W16D_ABL
+#define QG_W16D_ABL 0  // (tuning probes only) w16d_kernel ablation
+#endif
+template <int F, int RT, int NP> hipError_t w16d_launch_np(const GemmArgs& g, hipStream_t st) {
+    constexpr int W = QG_W16D_W;
+    using G = w16d_geom<F, RT, W, NP, QG_W16D_SB>;
+    auto k = w16d_kernel<F, RT, W, NP, QG_W16D_SB, QG_W16D_ABL>;
+    static std::atomic<unsigned long long> attr_done{0};
+    const hipError_t e = set_max_lds_once((const void*)k, (int)G::LDS, attr_done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((g.N + G::ROWS - 1) / G::ROWS, (g.M + 15) / 16), dim3(W * 64), G::LDS, st, (const float*)g.A,
+                       (const uint8_t*)g.B, g.C, g.M, g.N, g.K, (int)g.ldc_m, (int)g.ldc_n);
+    return hipGetLastError();
+}
+// 32-row tiles while they leave >= 256 workgroups, else 16-row ones
+inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
+template <int F> hipError_t w16d_launch(const GemmArgs& g, hipStream_t st) {
+    const bool rt2 = w16d_rt2(g);
+    if (w16s_parts(g.K) == 2) return rt2 ? w16d_launch_np<F, 2, 2>(g, st) : w16d_launch_np<F, 1, 2>(g, st);
+    return rt2 ? w16d_launch_np<F, 2, 3>(g, st) : w16d_launch_np<F, 1, 3>(g, st);
+}
+
 template <int F> hipError_t w16_dispatch(const GemmArgs& g, hipStream_t st) {
+    if constexpr (F == FMT_Q4_0 || F == FMT_Q8_0)
+        if (w16d_ok(g)) return w16d_launch<F>(g, st);
     if constexpr (F == FMT_Q4_0 || (F == FMT_Q8_0 && QG_W16S_Q8)) {
         // round-2 prefill: 16-B aligned activations and weights (rows are then 16-B multiples)
         if (((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0 && (g.M + 15) / 16 <= 65535) {
