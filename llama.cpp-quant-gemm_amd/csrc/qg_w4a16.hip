@@ -1282,28 +1282,40 @@ __global__ __launch_bounds__(W * 64, 1) void w16d_kernel(const float* __restrict
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             issue(h + G::NB * W, buf);
         }
+        // every split and decode first, then every MFMA (no VALU between the MFMAs: a VALU write into a
+        // register an in-flight MFMA still reads as its accumulator is a hazard, tests/test_isa_hazards.py)
+        u32x4_t ap[G::SB][NP], wf[G::SB][RT];
+        static_for<G::SB>([&](auto BI) {
+            constexpr int b = decltype(BI)::value;
+            if constexpr (NP == 2) {
+                w16_afrag2(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[b][0], ap[b][1]);
+            } else {
+                u32x4_t lo;
+                w16_afrag(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[b][0], ap[b][1], lo);
+                ap[b][NP - 1] = lo;
+            }
+#pragma unroll
+            for (int i = 0; i < RT; ++i) wf[b][i] = T::Q8 ? w16s_wfrag_q8(wv[b][i][0], wv[b][i][1]) : w16s_wfrag(wv[b][i][0]);
+        });
+        __builtin_amdgcn_sched_barrier(0);
         f32x4_t c[G::SB][RT];
         static_for<G::SB>([&](auto BI) {
             constexpr int b = decltype(BI)::value;
-            u32x4_t ap[NP];
-            if constexpr (NP == 2) {
-                w16_afrag2(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[0], ap[1]);
-            } else {
-                u32x4_t lo;
-                w16_afrag(__builtin_bit_cast(float4, xa[b][0]), __builtin_bit_cast(float4, xa[b][1]), ap[0], ap[1], lo);
-                ap[NP - 1] = lo;
-            }
 #pragma unroll
-            for (int i = 0; i < RT; ++i) {
-                const u32x4_t wf = T::Q8 ? w16s_wfrag_q8(wv[b][i][0], wv[b][i][1]) : w16s_wfrag(wv[b][i][0]);
-                c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[0]), __builtin_bit_cast(bf16x8_t, wf),
-                                                                  f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-                for (int pl = 1; pl < NP; ++pl)
-                    c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[pl]),
-                                                                      __builtin_bit_cast(bf16x8_t, wf), c[b][i], 0, 0, 0);
-            }
+            for (int i = 0; i < RT; ++i)
+                c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[b][0]),
+                                                                  __builtin_bit_cast(bf16x8_t, wf[b][i]), f32x4_t{0.f, 0.f, 0.f, 0.f},
+                                                                  0, 0, 0);
         });
+#pragma unroll
+        for (int pl = 1; pl < NP; ++pl)
+            static_for<G::SB>([&](auto BI) {
+                constexpr int b = decltype(BI)::value;
+#pragma unroll
+                for (int i = 0; i < RT; ++i)
+                    c[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ap[b][pl]),
+                                                                      __builtin_bit_cast(bf16x8_t, wf[b][i]), c[b][i], 0, 0, 0);
+            });
         // MFMA results read by the VALU behind an explicit wait (8 states needed; qg_mmq_kernel.hpp)
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
