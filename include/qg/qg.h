@@ -136,7 +136,11 @@ int qg_gemm_w8a8(const void* A_q8_1, const void* B_q8_0, float* C, int M, int N,
  * 2 (K + 2) 2^-24 sum_k |a_k w_k|; the high part is clamped to the largest finite bf16, so
  * activations up to FLT_MAX keep that bound and an infinite activation gives an infinite, not a NaN,
  * product). A: 4-B aligned floats (16-B for the fast path), any K % 32 == 0.
- * Prefill (M > 8, K % 256 == 0) splits K across workgroups when that fills the GPU; the partial
+ * 8 < M <= 32 with 16-B aligned A and B, K % 256 == 0, K <= 8192 and a grid of at most one workgroup
+ * per CU runs without split-K and without any workspace (round 4: each workgroup owns all of K; outputs
+ * deterministic); qg_gemm_w16_workspace_size still sizes the split-K route those shapes take when the
+ * operands are not 16-B aligned.
+ * Prefill (M > 8, K % 256 == 0) otherwise splits K across workgroups when that fills the GPU; the partial
  * tiles live in a workspace the library allocates once per (device, stream), on the first such
  * call outside stream capture. Calls made during stream capture never use the library's
  * workspace: they run without split-K (same results to fp32 summation order), so a graph holds
