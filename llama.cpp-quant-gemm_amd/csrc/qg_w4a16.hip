@@ -1626,8 +1626,8 @@ template <int F, int RT, int NP> hipError_t w16d_launch_np(const GemmArgs& g, hi
                        (const uint8_t*)g.B, g.C, g.M, g.N, g.K, (int)g.ldc_m, (int)g.ldc_n);
     return hipGetLastError();
 }
-// 32-row tiles while they leave >= 256 workgroups, else 16-row ones
-inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
+// 16-row tiles while their grid fits one dispatch round (<= 256 workgroups), else 32-row ones (w16d_ok)
+inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 15) / 16) * ((g.M + 15) / 16) > 256; }
 template <int F> hipError_t w16d_launch(const GemmArgs& g, hipStream_t st) {
     const bool rt2 = w16d_rt2(g);
     if (w16s_parts(g.K) == 2) return rt2 ? w16d_launch_np<F, 2, 2>(g, st) : w16d_launch_np<F, 1, 2>(g, st);

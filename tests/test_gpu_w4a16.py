@@ -168,7 +168,7 @@ def test_w16_library_workspace_two_threads_one_stream(O, qg):
 
     import torch
     lib = qg._lib.load()
-    shapes = [(32, 1024, 4096), (64, 8192, 4096)]
+    shapes = [(40, 1024, 4096), (64, 8192, 4096)]  # M > 32: both split K (M <= 32 runs w16d, no workspace)
     need = [lib.qg_gemm_w16_workspace_size(*s) for s in shapes]
     assert need[1] > max(need[0], 4 << 20)  # the second shape must grow the buffer past its first size
     data = []
