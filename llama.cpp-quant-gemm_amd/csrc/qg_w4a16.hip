@@ -1154,6 +1154,9 @@ __global__ __launch_bounds__(256) void w16s_kernel(const float* __restrict__ A, 
 // waits for the DMA), its weight row's qs dword q -> 8 exact bf16 of q - 8 (w16s_wfrag), NP chained
 // v_mfma_f32_16x16x32_bf16 per (block, row tile), acc += d_w * dot. The W partial tiles are summed in
 // fixed wave order through LDS at the end: deterministic, and the only global writes are the outputs.
+#ifndef QG_W16D_NB
+#define QG_W16D_NB 0  // (tuning knob) w16d_kernel stage slots per wave; 0: the most that fit, <= 3
+#endif
 // 32 bits at byte offset (compile-time OFF) of an LDS row, from aligned dword reads
 template <int OFF> __device__ __forceinline__ uint32_t w16_lds32(const uint8_t* base) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (OFF & ~3));
@@ -1179,11 +1182,12 @@ template <int F, int RT, int W, int NP, int SB_ = 2> struct w16d_geom {
     static constexpr int NI = (WP + AP + 63) / 64;         // DMA instructions per stage
     static constexpr int SBYTES = NI * 1024;
     static constexpr int AOFF = WP * 16;
-    static constexpr int NB = (160 * 1024) / (W * SBYTES) >= 3 ? 3 : 2;  // stage slots per wave
+    // stage slots per wave: QG_W16D_NB if set, else 3 when they fit, else 2
+    static constexpr int NB = QG_W16D_NB > 0 ? QG_W16D_NB : (160 * 1024) / (W * SBYTES) >= 3 ? 3 : 2;
     static constexpr int NACC = RT * 4;
     static constexpr size_t LDS = (size_t)W * NB * SBYTES;
-    static_assert(LDS <= 160 * 1024 && (size_t)W * NACC * 64 * 4 <= LDS, "LDS per workgroup");
-    static_assert((NB - 1) * NI <= 63, "vmcnt range");
+    static constexpr bool FITS = LDS <= 160 * 1024 && (size_t)W * NACC * 64 * 4 <= LDS;  // asserted by the kernel
+    static_assert(NB >= 1 && NB <= 3 && (NB - 1) * NI <= 63, "vmcnt range");
     static_assert(RIMG % 16 == 0 && ((RSB & 15) == 0 || (RSB & 15) == G16), "windows end inside the row");
 };
 
@@ -1193,6 +1197,7 @@ __global__ __launch_bounds__(W * 64, 1) void w16d_kernel(const float* __restrict
                                                          float* __restrict__ C, int M, int N, int K, int ldc_m, int ldc_n) {
     using G = w16d_geom<F, RT, W, NP, SB>;
     using T = wfmt<F>;
+    static_assert(G::FITS, "LDS per workgroup");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -1607,7 +1612,10 @@ inline bool w16d_ok(const GemmArgs& g) {
            (long)g.M * g.K * 4 < 0x7FFFFFF0L && (long)g.N * (g.K / QK) * wfmt<FMT_Q8_0>::BB < 0x7FFFFFF0L;  // buffer ranges
 }
 #ifndef QG_W16D_W
-#define QG_W16D_W 8  // waves per workgroup (tuning knob)
+// waves per workgroup: the most, up to this, whose two-slot rings fit the LDS — 12 for Q4_0, 11 for Q8_0
+// (profiles/r04_tuning/ab_w16d_waves.txt, M = 32: 8 waves with three slots 11.75 us, 12 waves with two
+// 10.78; M = 16 9.37 -> 8.54; more waves per SIMD overlap one wave's DMA wait with another's VALU)
+#define QG_W16D_W 12
 #endif
 #ifndef QG_W16D_SB
 #define QG_W16D_SB 2  // blocks per stage (tuning knob; 4 needs QG_W16D_W 4 for the LDS)
@@ -1616,7 +1624,10 @@ inline bool w16d_ok(const GemmArgs& g) {
 #define QG_W16D_ABL 0  // (tuning probes only) w16d_kernel ablation
 #endif
 template <int F, int RT, int NP> hipError_t w16d_launch_np(const GemmArgs& g, hipStream_t st) {
-    constexpr int W = QG_W16D_W;
+    constexpr int W = w16d_geom<F, RT, QG_W16D_W, NP, QG_W16D_SB>::FITS         ? QG_W16D_W
+                      : w16d_geom<F, RT, QG_W16D_W - 1, NP, QG_W16D_SB>::FITS ? QG_W16D_W - 1
+                      : w16d_geom<F, RT, QG_W16D_W - 2, NP, QG_W16D_SB>::FITS ? QG_W16D_W - 2
+                                                                             : 8;
     using G = w16d_geom<F, RT, W, NP, QG_W16D_SB>;
     auto k = w16d_kernel<F, RT, W, NP, QG_W16D_SB, QG_W16D_ABL>;
     static std::atomic<unsigned long long> attr_done{0};
