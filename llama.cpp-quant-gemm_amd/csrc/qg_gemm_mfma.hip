@@ -59,8 +59,20 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #ifndef QG_MMQ_RAW
 #define QG_MMQ_RAW 0
 #endif
+// (tuning knobs) waves and stage slots per wave of the M <= 32, 32-row tile
+#ifndef QG_MMQ_SMALL_W
+#define QG_MMQ_SMALL_W 8
+#endif
+#ifndef QG_MMQ_SMALL_NB
+#define QG_MMQ_SMALL_NB 2
+#endif
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;
+    if constexpr (BN == 32 && TT == 1 && W == 8 && (QG_MMQ_SMALL_W != 8 || QG_MMQ_SMALL_NB != 2)) {
+        constexpr int W2 = QG_MMQ_SMALL_W, NB2 = QG_MMQ_SMALL_NB;
+        if (g.sumi) return mmq_launch<F, BN, TT, W2, true, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
+        return mmq_launch<F, BN, TT, W2, false, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
+    }
     constexpr int E = (QG_MMQ_EARLY ? MMQ_EARLY : 0) | (QG_MMQ_RAW ? MMQ_RAW : 0);
     if constexpr (QG_MMQ_DYN && BN == 32 && TT == 1 && W == 8) {
         if (mmq_geom<F, BN, TT, W, P16, 2, 4, MMQ_DYN>::dyn_lds(g.K / QK / 4) <= 160 * 1024) {
