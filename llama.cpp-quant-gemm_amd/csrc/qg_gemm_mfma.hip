@@ -59,19 +59,30 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #ifndef QG_MMQ_RAW
 #define QG_MMQ_RAW 0
 #endif
-// (tuning knobs) waves and stage slots per wave of the M <= 32, 32-row tile
+// Waves and stage slots per wave of the M <= 32, 32-row x 16-token tile when its grid is one dispatch
+// round (<= 256 workgroups, one per CU): 12 waves with one stage each in flight beat 8 waves with two
+// (profiles/r04_tuning/ab_waves_r4v.txt: M = 32 6.91 -> 6.50 us, M = 24 6.72 -> 6.12, Q4_1 7.00 -> 6.77,
+// Q8_0 8.61 -> 8.43, M = 12 N = 8192 7.26 -> 6.98; more waves per SIMD overlap one wave's DMA wait with
+// another's compute). Grids of several rounds keep 8 x 2 (N = 11008: 14.7 vs 15.6 us). Falls back to
+// 8 x 2 where the rings would not fit the LDS.
 #ifndef QG_MMQ_SMALL_W
-#define QG_MMQ_SMALL_W 8
+#define QG_MMQ_SMALL_W 12
 #endif
 #ifndef QG_MMQ_SMALL_NB
-#define QG_MMQ_SMALL_NB 2
+#define QG_MMQ_SMALL_NB 1
 #endif
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;
     if constexpr (BN == 32 && TT == 1 && W == 8 && (QG_MMQ_SMALL_W != 8 || QG_MMQ_SMALL_NB != 2)) {
         constexpr int W2 = QG_MMQ_SMALL_W, NB2 = QG_MMQ_SMALL_NB;
-        if (g.sumi) return mmq_launch<F, BN, TT, W2, true, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
-        return mmq_launch<F, BN, TT, W2, false, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
+        constexpr bool fits = (size_t)W2 * NB2 * mmq_geom<F, BN, TT, W2, P16, NB2, 4>::BUF <= 160 * 1024 &&
+                              (size_t)W2 * BN / 16 * TT * 4 * 256 <= 160 * 1024;
+        if constexpr (fits) {
+            if ((long)((g.N + BN - 1) / BN) * ((g.M + 15) / 16) <= 256) {
+                if (g.sumi) return mmq_launch<F, BN, TT, W2, true, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
+                return mmq_launch<F, BN, TT, W2, false, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
+            }
+        }
     }
     constexpr int E = (QG_MMQ_EARLY ? MMQ_EARLY : 0) | (QG_MMQ_RAW ? MMQ_RAW : 0);
     if constexpr (QG_MMQ_DYN && BN == 32 && TT == 1 && W == 8) {

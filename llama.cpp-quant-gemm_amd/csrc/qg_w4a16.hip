@@ -1182,8 +1182,9 @@ template <int F, int RT, int W, int NP, int SB_ = 2> struct w16d_geom {
     static constexpr int NI = (WP + AP + 63) / 64;         // DMA instructions per stage
     static constexpr int SBYTES = NI * 1024;
     static constexpr int AOFF = WP * 16;
-    // stage slots per wave: QG_W16D_NB if set, else 3 when they fit, else 2
-    static constexpr int NB = QG_W16D_NB > 0 ? QG_W16D_NB : (160 * 1024) / (W * SBYTES) >= 3 ? 3 : 2;
+    // stage slots per wave: QG_W16D_NB if set, else the most that fit, at most 3
+    static constexpr int NBFIT = (160 * 1024) / (W * SBYTES);
+    static constexpr int NB = QG_W16D_NB > 0 ? QG_W16D_NB : NBFIT >= 3 ? 3 : NBFIT >= 1 ? NBFIT : 1;
     static constexpr int NACC = RT * 4;
     static constexpr size_t LDS = (size_t)W * NB * SBYTES;
     static constexpr bool FITS = LDS <= 160 * 1024 && (size_t)W * NACC * 64 * 4 <= LDS;  // asserted by the kernel
@@ -1612,10 +1613,13 @@ inline bool w16d_ok(const GemmArgs& g) {
            (long)g.M * g.K * 4 < 0x7FFFFFF0L && (long)g.N * (g.K / QK) * wfmt<FMT_Q8_0>::BB < 0x7FFFFFF0L;  // buffer ranges
 }
 #ifndef QG_W16D_W
-// waves per workgroup: the most, up to this, whose two-slot rings fit the LDS — 12 for Q4_0, 11 for Q8_0
-// (profiles/r04_tuning/ab_w16d_waves.txt, M = 32: 8 waves with three slots 11.75 us, 12 waves with two
-// 10.78; M = 16 9.37 -> 8.54; more waves per SIMD overlap one wave's DMA wait with another's VALU)
-#define QG_W16D_W 12
+// waves per workgroup (stage slots per wave: the most that fit): 16 waves with one slot each
+// (profiles/r04_tuning/ab_waves_r4v.txt, M = 32: 10.80 -> 10.15 us, M = 24 10.34 -> 9.52, M = 16
+// 8.54 -> 8.40, W8A16 10.81 -> 10.11, K = 8192 18.47 -> 17.57 against 12 waves with two slots, which beat
+// 8 waves with three: ab_w16d_waves.txt, 11.75 -> 10.78) — more waves per SIMD overlap one wave's DMA
+// wait with another's VALU; the refill of a wave's slot is issued right after its LDS reads, before the
+// stage's compute
+#define QG_W16D_W 16
 #endif
 #ifndef QG_W16D_SB
 #define QG_W16D_SB 2  // blocks per stage (tuning knob; 4 needs QG_W16D_W 4 for the LDS)
