@@ -71,14 +71,37 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #ifndef QG_MMQ_SMALL_NB
 #define QG_MMQ_SMALL_NB 1
 #endif
+// The same for the 16-row x 16-token tiles (M <= 16): 16 waves with one slot each where the grid is one
+// round (profiles/r04_tuning/ab_waves_r4y.txt, N = K = 4096: Q4_0 M = 16 5.45 -> 5.28 us, M = 8
+// 5.01 -> 4.82, M = 5 5.00 -> 4.77; Q4_1 M = 16 5.55 -> 5.36; Q5_0 M = 8 5.78 -> 5.34). Q8_0 keeps 8 x 2
+// (M = 16 6.58 -> 7.15 with 16 waves: its 34-byte blocks double the per-stage ingest). The 8-wave
+// 32 x 32 tiles (M > 32) keep 8 x 2: 12 or 16 waves exceed the VGPR budget of their accumulators
+// (ab_waves_r4x.txt: M = 64 9.8 -> 24-55 us).
+#ifndef QG_MMQ_S16_W
+#define QG_MMQ_S16_W 16
+#endif
+#ifndef QG_MMQ_S16_NB
+#define QG_MMQ_S16_NB 1
+#endif
+#ifndef QG_MMQ_L_W
+#define QG_MMQ_L_W 8
+#endif
+#ifndef QG_MMQ_L_NB
+#define QG_MMQ_L_NB 2
+#endif
+template <int F, int BN, int TT> constexpr bool alt_s16 = BN == 16 && F != FMT_Q8_0;
+template <int F, int BN, int TT>
+constexpr int alt_w = BN == 32 && TT == 1 ? QG_MMQ_SMALL_W : BN == 16 ? (alt_s16<F, BN, TT> ? QG_MMQ_S16_W : 8) : QG_MMQ_L_W;
+template <int F, int BN, int TT>
+constexpr int alt_nb = BN == 32 && TT == 1 ? QG_MMQ_SMALL_NB : BN == 16 ? (alt_s16<F, BN, TT> ? QG_MMQ_S16_NB : 2) : QG_MMQ_L_NB;
 template <int F, int BN, int TT, int W, bool P16> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W>;
-    if constexpr (BN == 32 && TT == 1 && W == 8 && (QG_MMQ_SMALL_W != 8 || QG_MMQ_SMALL_NB != 2)) {
-        constexpr int W2 = QG_MMQ_SMALL_W, NB2 = QG_MMQ_SMALL_NB;
+    if constexpr (W == 8 && (alt_w<F, BN, TT> != 8 || alt_nb<F, BN, TT> != 2)) {
+        constexpr int W2 = alt_w<F, BN, TT>, NB2 = alt_nb<F, BN, TT>;
         constexpr bool fits = (size_t)W2 * NB2 * mmq_geom<F, BN, TT, W2, P16, NB2, 4>::BUF <= 160 * 1024 &&
                               (size_t)W2 * BN / 16 * TT * 4 * 256 <= 160 * 1024;
         if constexpr (fits) {
-            if ((long)((g.N + BN - 1) / BN) * ((g.M + 15) / 16) <= 256) {
+            if ((long)((g.N + BN - 1) / BN) * ((g.M + 16 * TT - 1) / (16 * TT)) <= 256) {
                 if (g.sumi) return mmq_launch<F, BN, TT, W2, true, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
                 return mmq_launch<F, BN, TT, W2, false, P16, NB2, 0, false, 4, 1, true, 0, false>(g, st);
             }
