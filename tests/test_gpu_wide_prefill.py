@@ -57,3 +57,26 @@ def test_wide_prefill_strided_output_and_determinism(O, qg):
     assert bool((wide[:, :32] == -7.0).all()) and bool((wide[:, 32 + n:] == -7.0).all())
     for _ in range(3):
         assert torch.equal(qg.gemm_w4a8(a_d, b_d, m, n, k, t), dense)
+
+
+# The 16-row x 16-token tile of one-round grids (M <= 16): 16 waves with one stage slot each for every
+# format but Q8_0 (8 waves x 2 slots; qg_gemm_mfma.hip alt_w / alt_nb). Ragged M / N, one stage (4 blocks) to 192 blocks.
+S16_SHAPES = [(16, 4096, 4096), (8, 4096, 4096), (5, 4000, 2048), (13, 4088, 6144), (11, 2056, 128)]
+
+
+@pytest.mark.parametrize("t", WTYPES)
+@pytest.mark.parametrize("m,n,k", S16_SHAPES)
+def test_s16_prefill_exact(O, qg, t, m, n, k):
+    cfg = qg.debug_config(m, n, k, t)
+    if (m, n, k) in S16_SHAPES[:2]:
+        assert cfg.startswith(f"mmq F={t} BN=16 TT=1 "), cfg
+    if cfg.startswith(f"mmq F={t} BN=16 TT=1 ") and (n + 15) // 16 <= 256:
+        assert (" W=8 " in cfg and " NB=2 " in cfg) if t == 8 else (" W=16 " in cfg and " NB=1 " in cfg), cfg
+    _, _, aq, bq = make_case(O, m, n, k, t, seed=m + 3 * n)
+    a_d, b_d = dev(aq), dev(bq)
+    got = host(qg.debug_sumi(a_d, b_d, m, n, k, t, 2))
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(got, want)
+    c = host(qg.gemm_w4a8(a_d, b_d, m, n, k, t))
+    assert_close_to_oracle(O, c, aq, bq, t, mfma=True)
+    assert np.array_equal(c, host(qg.gemm_w4a8(a_d, b_d, m, n, k, t)))  # repeat: bit-identical
