@@ -527,6 +527,9 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMVG_TPW
 #define QG_GEMVG_TPW 2
 #endif
+#ifndef QG_GEMVG_WDIV
+#define QG_GEMVG_WDIV 2  // grouped launch workgroup size = the single launch's / QG_GEMVG_WDIV (below)
+#endif
 template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     constexpr int RPB = (WGS / 64) * (64 / LPR) * TPW;  // rows per workgroup
@@ -586,26 +589,44 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     }
     if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
         if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
-            GemvGroup grp = *static_cast<const GemvGroup*>(g.group);
-            const int rpw = one ? RPB * QG_GEMVG_TPW : RPB;  // rows per workgroup
-            int tiles = 0, tmin = INT32_MAX;
-            for (int i = 0; i < grp.count; ++i) {
-                const int t = (grp.it[i].N + rpw - 1) / rpw;
-                tiles = std::max(tiles, t);
-                tmin = std::min(tmin, t);
+            const GemvGroup& grp0 = *static_cast<const GemvGroup*>(g.group);
+            auto go = [&](auto GWc) -> hipError_t {
+                constexpr int GW = decltype(GWc)::value;
+                GemvGroup grp = grp0;
+                constexpr int RPBG = (GW / 64) * (64 / LPR);
+                const int rpw = one ? RPBG * QG_GEMVG_TPW : RPBG;  // rows per workgroup
+                int tiles = 0, tmin = INT32_MAX;
+                for (int i = 0; i < grp.count; ++i) {
+                    const int t = (grp.it[i].N + rpw - 1) / rpw;
+                    tiles = std::max(tiles, t);
+                    tmin = std::min(tmin, t);
+                }
+                auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, QG_GEMVG_TPW>
+                              : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false>;
+                if (lds > 64 * 1024) {
+                    hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                    if (e != hipSuccess) return e;
+                }
+                if (tiles == 0 || grp.count == 0) return hipSuccess;
+                const bool uniform = QG_GEMVG_XCD && tiles == tmin && grp.count % 8 == 0 && (long)tiles * grp.count <= INT32_MAX;
+                grp.tpi = uniform ? tiles : 0;
+                const dim3 grid = uniform ? dim3(tiles * grp.count) : dim3(tiles, grp.count);
+                hipLaunchKernelGGL(kg, grid, dim3(GW), lds, st, grp);
+                return hipGetLastError();
+            };
+            // workgroups of WGS / QG_GEMVG_WDIV threads while the largest item's rows fit one round of
+            // full-size workgroups (<= 256): twice as many resident per CU, so one workgroup's descriptor
+            // load and activation staging overlap another's weight stream (profiles/r04_tuning/
+            // ab_grouped_wgs_r4g2.txt, 64 items per launch, N = K = 4096: Q4_0 M = 1 1.541 -> 1.509 us per
+            // GEMV, M = 2 1.853 -> 1.688, M = 4 2.705 -> 2.494, Q8_0 2.885 -> 2.767; N = 11008 (344 tiles)
+            // 3.92 -> 4.01 with them, so larger items keep full-size workgroups)
+            if constexpr (QG_GEMVG_WDIV > 1 && WGS / QG_GEMVG_WDIV >= 64) {
+                const int rpw_full = one ? RPB * QG_GEMVG_TPW : RPB;
+                int nmax = 0;
+                for (int i = 0; i < grp0.count; ++i) nmax = std::max(nmax, grp0.it[i].N);
+                if ((nmax + rpw_full - 1) / rpw_full <= 256) return go(std::integral_constant<int, WGS / QG_GEMVG_WDIV>{});
             }
-            auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, WGS, PRE, true, QG_GEMVG_TPW>
-                          : gemvg_kernel<F, MT, BPL, LPR, WGS, PRE && (MT <= 2), false>;
-            if (lds > 64 * 1024) {
-                hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                if (e != hipSuccess) return e;
-            }
-            if (tiles == 0 || grp.count == 0) return hipSuccess;
-            const bool uniform = QG_GEMVG_XCD && tiles == tmin && grp.count % 8 == 0 && (long)tiles * grp.count <= INT32_MAX;
-            grp.tpi = uniform ? tiles : 0;
-            const dim3 grid = uniform ? dim3(tiles * grp.count) : dim3(tiles, grp.count);
-            hipLaunchKernelGGL(kg, grid, dim3(WGS), lds, st, grp);
-            return hipGetLastError();
+            return go(std::integral_constant<int, WGS>{});
         }
     }
     if (m1) {

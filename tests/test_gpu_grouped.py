@@ -165,3 +165,21 @@ def test_grouped_argument_checks(qg):
     arr[0] = qg._GemvItem(256, 256, 256, 16, 8)
     assert lib.qg_gemm_w4a8_grouped(arr, 1, 1, 4096, 2, st) == -1    # ldc < N
     assert lib.qg_gemm_w4a8_grouped(arr, -1, 1, 4096, 2, st) == -1
+
+
+@pytest.mark.parametrize("ns", [[11008, 4096, 100], [8200, 17, 4096], [4096, 4096, 4096, 4096], [33, 1, 7]])
+@pytest.mark.parametrize("t,m", [(2, 1), (2, 4), (8, 2), (7, 1)])
+def test_grouped_workgroup_size_split(O, qg, ns, t, m):
+    """Groups whose largest item fits one round of full-size workgroups launch half-size ones
+    (qg_gemv_kernel.hpp, QG_GEMVG_WDIV), larger ones full-size: every item bit-identical to its
+    single launch either way."""
+    rng = np.random.default_rng(sum(ns) + 10 * t + m)
+    k = 2048
+    aqs, bqs = _case(O, rng, m, ns, k, t, shared=False)
+    a_d = [dev(a) for a in aqs]
+    b_d = [dev(b) for b in bqs]
+    outs = qg.gemm_w4a8_grouped(a_d, b_d, ns, m, k, t)
+    for i, n in enumerate(ns):
+        single = host(qg.gemm_w4a8(a_d[i], b_d[i], m, n, k, t))
+        assert np.array_equal(host(outs[i]).view(np.uint32), single.view(np.uint32)), f"item {i}"
+    close_to_oracle(O, host(outs[-1]), aqs[-1], bqs[-1], t)

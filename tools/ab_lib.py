@@ -32,7 +32,13 @@ def load(path: str) -> ctypes.CDLL:
     lib.qg_gemm_w4a8_ex.restype = ctypes.c_int
     lib.qg_gemm_w4a16_ws.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_size_t, P]
     lib.qg_gemm_w4a16_ws.restype = ctypes.c_int
+    lib.qg_gemm_w4a8_grouped.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    lib.qg_gemm_w4a8_grouped.restype = ctypes.c_int
     return lib
+
+
+class GemvItem(ctypes.Structure):  # qg_gemv_item (include/qg/qg.h)
+    _fields_ = [("A_q8_1", P), ("B", P), ("C", P), ("N", ctypes.c_int), ("ldc", ctypes.c_int)]
 
 
 def main() -> None:
@@ -46,6 +52,7 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--w16", action="store_true", help="time qg_gemm_w4a16 (fp32 activations, Q4_0 weights)")
+    ap.add_argument("--grouped", action="store_true", help="one qg_gemm_w4a8_grouped launch of the G GEMVs per step")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     algos = [a.algo] * len(libs)
@@ -73,6 +80,11 @@ def main() -> None:
         wss = [torch.zeros(WSB // 4, dtype=torch.int32, device=dev) for _ in libs] if a.w16 else []
         for li, lib in enumerate(libs):
             def step(st, li=li, lib=lib):
+                if a.grouped:
+                    items = (GemvItem * a.G)(*[GemvItem(aq.data_ptr(), copies[j % R].data_ptr(), outs[li, j].data_ptr(), N, 0)
+                                               for j in range(a.G)])
+                    assert lib.qg_gemm_w4a8_grouped(items, a.G, M, K, wt, st) == 0
+                    return
                 for j in range(a.G):
                     if a.w16:
                         rc = lib.qg_gemm_w4a16_ws(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
