@@ -654,6 +654,26 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     }
     // PRE beyond MT = 2 only in the loop-free form (with the unit loop it spills at MT = 4); a strided
     // batch of loop-free GEMVs takes QG_GEMV_TPW row tiles per workgroup (same per-row arithmetic)
+// A strided batch of loop-free GEMVs whose N fits one round of full-size workgroups runs half-size
+// ones, as the grouped launch (profiles/r04_tuning/ab_batched_wgs_r4b.txt, 64 products per launch,
+// N = K = 4096: Q4_0 M = 1 1.526 -> 1.478 us per GEMV, M = 2 1.772 -> 1.641, M = 4 3.32 -> 2.76,
+// N = 1024 0.436 -> 0.421; Q5_0 / Q8_0 M = 1 within +-0.7 %)
+#ifndef QG_GEMVB_WDIV
+#define QG_GEMVB_WDIV 2
+#endif
+    if constexpr (QG_GEMVB_WDIV > 1 && WGS / QG_GEMVB_WDIV >= 64 && !SUMI && !NT) {
+        constexpr int GW = WGS / QG_GEMVB_WDIV, RPBB = (GW / 64) * (64 / LPR) * QG_GEMV_TPW;
+        if (one && g.batch > 1 && grid <= 256) {
+            auto kb = gemv_kernel<F, MT, BPL, LPR, GW, SUMI, AIN, NT, PRE, true, 0, QG_GEMV_TPW>;
+            if (lds > 64 * 1024) {
+                hipError_t e = hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kb, dim3((g.N + RPBB - 1) / RPBB, g.batch), dim3(GW), lds, st, (const uint32_t*)g.A,
+                               (const uint8_t*)g.B, g.sA, g.sB, g.M, g.N, g.K, g.C, g.sC, g.ldc_m, g.ldc_n, g.sumi);
+            return hipGetLastError();
+        }
+    }
     constexpr bool tpw_ok = !SUMI && !NT && QG_GEMV_TPW > 1;
     const bool multi = tpw_ok && one && g.batch > 1;
     auto kfn = multi ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true, 0, tpw_ok ? QG_GEMV_TPW : 1>

@@ -213,6 +213,22 @@ def test_strided_batched(O, qg, m, t):
         assert_close_to_oracle(O, out[i], a[i], b[i], t)
 
 
+@pytest.mark.parametrize("m,n,k,t", [(1, 4096, 4096, 2), (2, 1000, 1024, 2), (4, 4096, 2048, 2), (1, 4096, 4096, 8),
+                                     (1, 17, 4096, 6), (3, 8200, 4096, 2)])
+def test_strided_batched_bit_identical(O, qg, m, n, k, t):
+    """The strided batch (half-size workgroups where N fits one round, qg_gemv_kernel.hpp QG_GEMVB_WDIV;
+    full-size beyond) is bit-identical, item by item, to the single launch."""
+    nbatch = 3
+    items = [make_case(O, m, n, k, t, seed=200 + i) for i in range(nbatch)]
+    a = np.stack([it[2] for it in items])
+    b = np.stack([it[3] for it in items])
+    out = host(qg.gemm_w4a8_batched(dev(a), dev(b), m, n, k, t))
+    for i in range(nbatch):
+        single = host(qg.gemm_w4a8(dev(a[i]), dev(b[i]), m, n, k, t))
+        assert np.array_equal(out[i].view(np.uint32), single.view(np.uint32)), f"item {i}"
+    assert_close_to_oracle(O, out[-1], a[-1], b[-1], t)
+
+
 @pytest.mark.parametrize("m,n,k", [(1, 1, 32), (1, 3, 96), (2, 7, 288), (4, 65, 4128), (1, 4097, 256),
                                    (9, 33, 512), (16, 64, 1024), (1, 5, 14336), (3, 17, 8192)])
 def test_auto_dispatch_shapes(O, qg, m, n, k):

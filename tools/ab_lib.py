@@ -34,6 +34,9 @@ def load(path: str) -> ctypes.CDLL:
     lib.qg_gemm_w4a16_ws.restype = ctypes.c_int
     lib.qg_gemm_w4a8_grouped.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     lib.qg_gemm_w4a8_grouped.restype = ctypes.c_int
+    I64 = ctypes.c_int64
+    lib.qg_gemm_w4a8_strided_batched.argtypes = [P, I64, P, I64, P, I64] + [ctypes.c_int] * 5 + [P]
+    lib.qg_gemm_w4a8_strided_batched.restype = ctypes.c_int
     return lib
 
 
@@ -53,6 +56,7 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--w16", action="store_true", help="time qg_gemm_w4a16 (fp32 activations, Q4_0 weights)")
     ap.add_argument("--grouped", action="store_true", help="one qg_gemm_w4a8_grouped launch of the G GEMVs per step")
+    ap.add_argument("--batched", action="store_true", help="one qg_gemm_w4a8_strided_batched launch of the G GEMVs per step")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     algos = [a.algo] * len(libs)
@@ -80,6 +84,11 @@ def main() -> None:
         wss = [torch.zeros(WSB // 4, dtype=torch.int32, device=dev) for _ in libs] if a.w16 else []
         for li, lib in enumerate(libs):
             def step(st, li=li, lib=lib):
+                if a.batched:
+                    assert R >= a.G
+                    assert lib.qg_gemm_w4a8_strided_batched(P(aq.data_ptr()), 0, P(copies.data_ptr()), copies[0].numel(),
+                                                            P(outs[li].data_ptr()), M * N, a.G, M, N, K, wt, st) == 0
+                    return
                 if a.grouped:
                     items = (GemvItem * a.G)(*[GemvItem(aq.data_ptr(), copies[j % R].data_ptr(), outs[li, j].data_ptr(), N, 0)
                                                for j in range(a.G)])
