@@ -527,6 +527,17 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMVG_TPW
 #define QG_GEMVG_TPW 2
 #endif
+// M >= 2 grouped / strided-batch launches whose items fit one round: 256-thread workgroups of two row
+// tiles (profiles/r04_tuning/ab_mt_wgs_r4m.txt, 64 products per launch, N = K = 4096, vs the M = 1 rule:
+// strided Q4_0 M = 2 1.72 -> 1.64 us, M = 4 2.78 -> 2.42, Q4_1 M = 3 3.54 -> 2.59; grouped Q4_0 M = 2
+// 1.75 -> 1.61, M = 4 2.49 -> 2.41; Q5_x / Q8_0 within +-1 % except grouped Q8_0 M = 4 +2 %; one row tile
+// per 256-thread workgroup is slower everywhere). 0: the M = 1 rule.
+#ifndef QG_GEMV_MTGW
+#define QG_GEMV_MTGW 256
+#endif
+#ifndef QG_GEMV_MTTPW
+#define QG_GEMV_MTTPW 2
+#endif
 #ifndef QG_GEMVG_WDIV
 #define QG_GEMVG_WDIV 2  // grouped launch workgroup size = the single launch's / QG_GEMVG_WDIV (below)
 #endif
@@ -590,18 +601,18 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
         if (g.group) {  // grouped launch (qg_gemm_w4a8_grouped): blockIdx.y = item
             const GemvGroup& grp0 = *static_cast<const GemvGroup*>(g.group);
-            auto go = [&](auto GWc) -> hipError_t {
-                constexpr int GW = decltype(GWc)::value;
+            auto go = [&](auto GWc, auto TPc) -> hipError_t {
+                constexpr int GW = decltype(GWc)::value, TP = decltype(TPc)::value;
                 GemvGroup grp = grp0;
                 constexpr int RPBG = (GW / 64) * (64 / LPR);
-                const int rpw = one ? RPBG * QG_GEMVG_TPW : RPBG;  // rows per workgroup
+                const int rpw = one ? RPBG * TP : RPBG;  // rows per workgroup
                 int tiles = 0, tmin = INT32_MAX;
                 for (int i = 0; i < grp.count; ++i) {
                     const int t = (grp.it[i].N + rpw - 1) / rpw;
                     tiles = std::max(tiles, t);
                     tmin = std::min(tmin, t);
                 }
-                auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, QG_GEMVG_TPW>
+                auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP>
                               : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false>;
                 if (lds > 64 * 1024) {
                     hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -620,13 +631,17 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
             // ab_grouped_wgs_r4g2.txt, 64 items per launch, N = K = 4096: Q4_0 M = 1 1.541 -> 1.509 us per
             // GEMV, M = 2 1.853 -> 1.688, M = 4 2.705 -> 2.494, Q8_0 2.885 -> 2.767; N = 11008 (344 tiles)
             // 3.92 -> 4.01 with them, so larger items keep full-size workgroups)
-            if constexpr (QG_GEMVG_WDIV > 1 && WGS / QG_GEMVG_WDIV >= 64) {
+            constexpr bool MTW = QG_GEMV_MTGW > 0 && MT >= 2;
+            constexpr int GWH = MTW ? (QG_GEMV_MTGW < WGS ? QG_GEMV_MTGW : WGS) : WGS / QG_GEMVG_WDIV;
+            constexpr int TPH = MTW ? QG_GEMV_MTTPW : QG_GEMVG_TPW;
+            if constexpr (GWH < WGS && GWH >= 64) {
                 const int rpw_full = one ? RPB * QG_GEMVG_TPW : RPB;
                 int nmax = 0;
                 for (int i = 0; i < grp0.count; ++i) nmax = std::max(nmax, grp0.it[i].N);
-                if ((nmax + rpw_full - 1) / rpw_full <= 256) return go(std::integral_constant<int, WGS / QG_GEMVG_WDIV>{});
+                if ((nmax + rpw_full - 1) / rpw_full <= 256)
+                    return go(std::integral_constant<int, GWH>{}, std::integral_constant<int, TPH>{});
             }
-            return go(std::integral_constant<int, WGS>{});
+            return go(std::integral_constant<int, WGS>{}, std::integral_constant<int, QG_GEMVG_TPW>{});
         }
     }
     if (m1) {
@@ -661,10 +676,13 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
 #ifndef QG_GEMVB_WDIV
 #define QG_GEMVB_WDIV 2
 #endif
-    if constexpr (QG_GEMVB_WDIV > 1 && WGS / QG_GEMVB_WDIV >= 64 && !SUMI && !NT) {
-        constexpr int GW = WGS / QG_GEMVB_WDIV, RPBB = (GW / 64) * (64 / LPR) * QG_GEMV_TPW;
+    constexpr bool MTB = QG_GEMV_MTGW > 0 && MT >= 2;
+    constexpr int GWB = MTB ? (QG_GEMV_MTGW < WGS ? QG_GEMV_MTGW : WGS) : WGS / QG_GEMVB_WDIV;
+    constexpr int TPB = MTB ? QG_GEMV_MTTPW : QG_GEMV_TPW;
+    if constexpr (GWB < WGS && GWB >= 64 && !SUMI && !NT) {
+        constexpr int GW = GWB, RPBB = (GW / 64) * (64 / LPR) * TPB;
         if (one && g.batch > 1 && grid <= 256) {
-            auto kb = gemv_kernel<F, MT, BPL, LPR, GW, SUMI, AIN, NT, PRE, true, 0, QG_GEMV_TPW>;
+            auto kb = gemv_kernel<F, MT, BPL, LPR, GW, SUMI, AIN, NT, PRE, true, 0, TPB>;
             if (lds > 64 * 1024) {
                 hipError_t e = hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
