@@ -1622,18 +1622,19 @@ inline bool w16d_ok(const GemmArgs& g) {
 #define QG_W16D_W 16
 #endif
 #ifndef QG_W16D_SB
-#define QG_W16D_SB 2  // blocks per stage (tuning knob; 4 needs QG_W16D_W 4 for the LDS)
+#define QG_W16D_SB 2  // blocks per stage (tuning knob; Q4_0 from K = QG_W16D_SB4_MINK takes 4, w16d_launch)
 #endif
 #ifndef QG_W16D_ABL
 #define QG_W16D_ABL 0  // (tuning probes only) w16d_kernel ablation
 #endif
-template <int F, int RT, int NP> hipError_t w16d_launch_np(const GemmArgs& g, hipStream_t st) {
-    constexpr int W = w16d_geom<F, RT, QG_W16D_W, NP, QG_W16D_SB>::FITS         ? QG_W16D_W
-                      : w16d_geom<F, RT, QG_W16D_W - 1, NP, QG_W16D_SB>::FITS ? QG_W16D_W - 1
-                      : w16d_geom<F, RT, QG_W16D_W - 2, NP, QG_W16D_SB>::FITS ? QG_W16D_W - 2
-                                                                             : 8;
-    using G = w16d_geom<F, RT, W, NP, QG_W16D_SB>;
-    auto k = w16d_kernel<F, RT, W, NP, QG_W16D_SB, QG_W16D_ABL>;
+template <int F, int RT, int NP, int SB = QG_W16D_SB, int WREQ = QG_W16D_W>
+hipError_t w16d_launch_np(const GemmArgs& g, hipStream_t st) {
+    constexpr int W = w16d_geom<F, RT, WREQ, NP, SB>::FITS         ? WREQ
+                      : w16d_geom<F, RT, WREQ - 1, NP, SB>::FITS ? WREQ - 1
+                      : w16d_geom<F, RT, WREQ - 2, NP, SB>::FITS ? WREQ - 2
+                                                                 : 8;
+    using G = w16d_geom<F, RT, W, NP, SB>;
+    auto k = w16d_kernel<F, RT, W, NP, SB, QG_W16D_ABL>;
     static std::atomic<unsigned long long> attr_done{0};
     const hipError_t e = set_max_lds_once((const void*)k, (int)G::LDS, attr_done);
     if (e != hipSuccess) return e;
@@ -1643,8 +1644,21 @@ template <int F, int RT, int NP> hipError_t w16d_launch_np(const GemmArgs& g, hi
 }
 // 16-row tiles while their grid fits one dispatch round (<= 256 workgroups), else 32-row ones (w16d_ok)
 inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 15) / 16) * ((g.M + 15) / 16) > 256; }
+// Q4_0 from K = 4096 (>= 32 four-block stages, so each of 12 waves takes two or three): 4-block stages
+// with 12 waves (profiles/r04_tuning/ab_w16d_sb4*.txt: M = 32 10.12 -> 9.90 us, M = 16 8.38 -> 8.19,
+// M = 12 8.20 -> 8.06, K = 8192 17.54 -> 17.25, M = 20 / 24 +0.8 / +1.3 %; K = 1024 +8 %: 8 stages for 12
+// waves). The longer 72-B weight windows take fewer DMA requests per byte.
+#ifndef QG_W16D_SB4_MINK
+#define QG_W16D_SB4_MINK 4096
+#endif
 template <int F> hipError_t w16d_launch(const GemmArgs& g, hipStream_t st) {
     const bool rt2 = w16d_rt2(g);
+    if constexpr (F == FMT_Q4_0 && QG_W16D_SB4_MINK > 0 && QG_W16D_SB == 2) {
+        if (g.K >= QG_W16D_SB4_MINK) {
+            if (w16s_parts(g.K) == 2) return rt2 ? w16d_launch_np<F, 2, 2, 4, 12>(g, st) : w16d_launch_np<F, 1, 2, 4, 12>(g, st);
+            return rt2 ? w16d_launch_np<F, 2, 3, 4, 12>(g, st) : w16d_launch_np<F, 1, 3, 4, 12>(g, st);
+        }
+    }
     if (w16s_parts(g.K) == 2) return rt2 ? w16d_launch_np<F, 2, 2>(g, st) : w16d_launch_np<F, 1, 2>(g, st);
     return rt2 ? w16d_launch_np<F, 2, 3>(g, st) : w16d_launch_np<F, 1, 3>(g, st);
 }
