@@ -32,6 +32,8 @@ def load(path: str) -> ctypes.CDLL:
     lib.qg_gemm_w4a8_ex.restype = ctypes.c_int
     lib.qg_gemm_w4a16_ws.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_size_t, P]
     lib.qg_gemm_w4a16_ws.restype = ctypes.c_int
+    lib.qg_gemm_w8a16.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    lib.qg_gemm_w8a16.restype = ctypes.c_int
     lib.qg_gemm_w4a8_grouped.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     lib.qg_gemm_w4a8_grouped.restype = ctypes.c_int
     I64 = ctypes.c_int64
@@ -95,7 +97,10 @@ def main() -> None:
                     assert lib.qg_gemm_w4a8_grouped(items, a.G, M, K, wt, st) == 0
                     return
                 for j in range(a.G):
-                    if a.w16:
+                    if a.w16 and wt == 8:
+                        rc = lib.qg_gemm_w8a16(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
+                                               P(outs[li, j].data_ptr()), M, N, K, st)
+                    elif a.w16:
                         rc = lib.qg_gemm_w4a16_ws(P(aq.data_ptr()), P(copies[j % R].data_ptr()),
                                                   P(outs[li, j].data_ptr()), M, N, K, P(wss[li].data_ptr()), WSB, st)
                     else:
