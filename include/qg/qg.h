@@ -105,8 +105,9 @@ int qg_gemm_w4a8_ws(const void* A_q8_1, const void* B, float* C, int M, int N, i
  * qg_gemm_w4a8_prepacked then computes the SAME product as qg_gemm_w4a8(A, B, ...) (within the
  * summation-order bound; K is the logical K) from B_packed: the activations are padded into
  * `workspace` (>= qg_gemm_w4a8_prepacked_workspace_size(M, K) bytes, 16-B aligned; 0 when K/32 is
- * already a multiple of 8) and the QG_ALGO_AUTO kernel runs on K' — no per-call weight copy.
- * Capture-safe. */
+ * already a multiple of 8) and the QG_ALGO_AUTO kernel runs on K' — no per-call weight copy. From M = 5
+ * (the MFMA kernel) the activations are read in place instead (round 5: one launch, the workspace
+ * is not touched). Capture-safe. */
 size_t qg_repack_weights_bytes(int N, int K, int wtype);
 int qg_repack_weights(const void* B, void* B_packed, int N, int K, int wtype, qg_stream_t stream);
 size_t qg_gemm_w4a8_prepacked_workspace_size(int M, int K);
@@ -119,6 +120,31 @@ int qg_gemm_w4a8_padded(const void* A_padded, const void* B_packed, float* C, in
                         qg_stream_t stream);
 int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, int M, int N, int K, int wtype,
                            void* workspace, size_t workspace_bytes, qg_stream_t stream);
+
+/* Load-time TILED weight layout (round 5) — the fast form for weights used many times, any K % 32 == 0.
+ * qg_tile_weights writes B_tiled (16-B aligned, qg_tile_weights_bytes(N, K, wtype) bytes) from B
+ * [N][K/32]: rows in tiles of 32, K/32 in stages of 4 blocks, each (tile, stage) one contiguous run of
+ * 128 * block_bytes bytes whose fields are arranged in the prefill kernel's operand order (qs by MFMA
+ * k-slot, then qh, then the f16 scales); rows past N and blocks past K/32 are zero (d = 0: an exact +0
+ * term). The layout is specified in llama.cpp-quant-gemm_amd/csrc/qg_mmq_kernel.hpp (tiled_fmt) and
+ * restated in oracle/oracle.py (tile_weights); one streaming kernel.
+ * qg_gemm_w4a8_tiled then computes the same product as qg_gemm_w4a8(A, B, ...) (activation-major,
+ * A: block_q8_1 [M][K/32], 16-B aligned; within the reassociation bound of the MFMA kernel, DESIGN.md
+ * §5) from B_tiled in ONE launch for every M — the prefill's weight stages are one linear stream
+ * instead of 32 row segments. K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
+ * activation rows). _ldc: output row stride (>= N floats). qg_debug_sumi_tiled / qg_debug_config_tiled
+ * are the parity hook and the configuration query of the same instantiation (as qg_debug_sumi /
+ * qg_debug_config below). Replaces the tiled-GEMM role of include/gemm_cuda_tiled.cuh:293-300 and the
+ * cp.async-staged kernels/gemm/gemm_async_copy.cuh:65-232 for reused weights. */
+size_t qg_tile_weights_bytes(int N, int K, int wtype);
+int qg_tile_weights(const void* B, void* B_tiled, int N, int K, int wtype, qg_stream_t stream);
+int qg_gemm_w4a8_tiled(const void* A_q8_1, const void* B_tiled, float* C, int M, int N, int K, int wtype,
+                       qg_stream_t stream);
+int qg_gemm_w4a8_tiled_ldc(const void* A_q8_1, const void* B_tiled, float* C, int M, int N, int K, int64_t ldc,
+                           int wtype, qg_stream_t stream);
+int qg_debug_sumi_tiled(const void* A_q8_1, const void* B_tiled, int32_t* sumi, int M, int N, int K, int wtype,
+                        qg_stream_t stream);
+int qg_debug_config_tiled(int M, int N, int K, int wtype, int sumi, char* buf, size_t len);
 
 /* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
  * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of

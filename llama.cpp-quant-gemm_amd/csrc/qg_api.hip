@@ -206,6 +206,19 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     return QG_OK;
 }
 
+// The tiled weight layout (qg_tile_weights): the MFMA kernel for every M (LAY_TILED; odd K/32 through
+// its activation windows).
+int run_tiled(GemmArgs& g, hipStream_t st) {
+    if (g.M < 0 || g.N < 0) return QG_ERR_INVALID_ARG;
+    if (g.K <= 0 || g.K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(g.wtype)) return QG_ERR_UNSUPPORTED;
+    if (g.M == 0 || g.N == 0) return QG_OK;
+    if (!g.A || !g.B || (!g.C && !g.sumi)) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 15) != 0) return QG_ERR_ALIGN;
+    if (!mfma_eligible(g)) return QG_ERR_UNSUPPORTED;
+    return hip_status(launch_mfma(g, st));
+}
+
 int block_bytes(int t) {
     switch (t) {
         case QG_TYPE_Q4_0: return 18;
@@ -462,7 +475,15 @@ int qg_gemm_w4a8_prepacked(const void* A, const void* B_packed, float* C, int M,
     GemmArgs g;
     g.A = A; g.B = B_packed; g.C = C; g.M = M; g.N = N; g.K = nbp * 32; g.wtype = wtype;
     g.ldc_m = N; g.ldc_n = 1;
-    if (nbp != K / 32) {  // activations padded into the caller's workspace, same zero blocks
+    if (nbp != K / 32) {
+        // round 5: where the MFMA kernel runs (M >= 5), it reads the plain activation rows itself
+        // (activation windows against the padded weight rows, qg_mmq_kernel.hpp AW): one launch, no
+        // workspace touched
+        GemmArgs w = g;
+        w.K = K;
+        w.nbw = nbp;
+        if (M > 4 && mfma_eligible(w)) return hip_status(launch_mfma(w, st));
+        // otherwise the activations are padded into the caller's workspace, same zero blocks
         if (!workspace || workspace_bytes < qg_gemm_w4a8_prepacked_workspace_size(M, K)) return QG_ERR_INVALID_ARG;
         if (((uintptr_t)A & 1) != 0 || ((uintptr_t)workspace & 15) != 0) return QG_ERR_ALIGN;
         const hipError_t e = launch_pad_rows(A, workspace, M, (K / 32) * 36, nbp * 36, st);
@@ -470,6 +491,57 @@ int qg_gemm_w4a8_prepacked(const void* A, const void* B_packed, float* C, int M,
         g.A = workspace;
     }
     return run_gemm(g, QG_ALGO_AUTO, st);
+}
+
+size_t qg_tile_weights_bytes(int N, int K, int wtype) {
+    if (N < 0 || K <= 0 || K % 32 != 0 || !is_weight_type(wtype)) return 0;
+    return tiled_weight_bytes(N, K, wtype);
+}
+
+int qg_tile_weights(const void* B, void* B_tiled, int N, int K, int wtype, qg_stream_t stream) {
+    if (N < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (!is_weight_type(wtype)) return QG_ERR_UNSUPPORTED;
+    if (N == 0) return QG_OK;
+    if (!B || !B_tiled) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)B & 1) != 0 || ((uintptr_t)B_tiled & 15) != 0) return QG_ERR_ALIGN;
+    return hip_status(launch_tile_weights(B, B_tiled, N, K, wtype, (hipStream_t)stream));
+}
+
+int qg_gemm_w4a8_tiled_ldc(const void* A, const void* B_tiled, float* C, int M, int N, int K, int64_t ldc, int wtype,
+                           qg_stream_t stream) {
+    if (ldc < N || (M > 1 && ldc <= 0)) return QG_ERR_INVALID_ARG;
+    GemmArgs g;
+    g.A = A; g.B = B_tiled; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = (long)ldc; g.ldc_n = 1;
+    g.lay = LAY_TILED;
+    return run_tiled(g, (hipStream_t)stream);
+}
+
+int qg_gemm_w4a8_tiled(const void* A, const void* B_tiled, float* C, int M, int N, int K, int wtype, qg_stream_t stream) {
+    return qg_gemm_w4a8_tiled_ldc(A, B_tiled, C, M, N, K, N, wtype, stream);
+}
+
+int qg_debug_sumi_tiled(const void* A, const void* B_tiled, int32_t* sumi, int M, int N, int K, int wtype,
+                        qg_stream_t stream) {
+    GemmArgs g;
+    g.A = A; g.B = B_tiled; g.sumi = sumi; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.lay = LAY_TILED;
+    return run_tiled(g, (hipStream_t)stream);
+}
+
+int qg_debug_config_tiled(int M, int N, int K, int wtype, int sumi, char* buf, size_t len) {
+    if (!buf || len == 0) return QG_ERR_INVALID_ARG;
+    buf[0] = 0;
+    GemmArgs g;
+    g.A = (const void*)256; g.B = (const void*)256; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    if (sumi) g.sumi = (int32_t*)256;
+    else g.C = (float*)256;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.lay = LAY_TILED;
+    g.describe = buf; g.describe_len = len;
+    return run_tiled(g, nullptr);
 }
 
 int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int wtype, qg_stream_t stream) {

@@ -11,12 +11,19 @@ namespace qg {
 // Activation input of a product: Q8_1 blocks, or FP32 / FP16 rows quantized inside the kernel.
 enum : int { AIN_Q8_1 = 0, AIN_F32 = 1, AIN_F16_FUSED = 2 };
 
+// Weight layouts of the MFMA kernel (qg_mmq_kernel.hpp): the reference's rows, or qg_tile_weights' tiles.
+enum : int { LAY_ROWS = 0, LAY_TILED = 1 };
+
 // One W4A8 product C = A_q8_1 * B_w^T, activation-major indices (m = activation row, n = weight
 // row); the output element (m, n) lives at C[m * ldc_m + n * ldc_n].
 struct GemmArgs {
     const void* A = nullptr;     // block_q8_1 [M][K/32] (ain == AIN_Q8_1), else float/half [M][K]
     int ain = AIN_Q8_1;
-    const void* B = nullptr;     // weight blocks [N][K/32] of type wtype
+    const void* B = nullptr;     // weight blocks [N][K/32] of type wtype (lay = LAY_ROWS), or the
+                                 // qg_tile_weights layout (lay = LAY_TILED, qg_mmq_kernel.hpp)
+    int lay = 0;                 // weight layout: 0 the reference's rows, 1 tiled
+    int nbw = 0;                 // LAY_ROWS: weight blocks per row when it differs from K/32 (the
+                                 // qg_repack_weights rows of qg_gemm_w4a8_prepacked), else 0
     float* C = nullptr;
     int32_t* sumi = nullptr;     // debug: per-block int32 dots [M][N][K/32] instead of C
     int M = 0, N = 0, K = 0;
@@ -95,6 +102,10 @@ size_t repack_workspace_bytes(const GemmArgs& g);  // padded weights + activatio
 // Weights [N][K/32] -> rows of K'/32 = round_up(K/32, 8) blocks, zero blocks after the real ones
 // (qg_repack_weights); activations the same (qg_gemm_w4a8_prepacked). Both enqueue one kernel.
 int padded_blocks(int K);
+// Weights [N][K/32] -> the tiled layout (qg_tile_weights; tiled_fmt in qg_mmq_kernel.hpp): rows in
+// tiles of 32, K/32 in stages of 4 blocks, zero blocks / rows as padding. One kernel.
+size_t tiled_weight_bytes(int N, int K, int wtype);
+hipError_t launch_tile_weights(const void* B, void* B_tiled, int N, int K, int wtype, hipStream_t st);
 hipError_t launch_pad_rows(const void* src, void* dst, long rows, int row_bytes, int padded_row_bytes, hipStream_t st);
 
 // W4A16 / W8A16: FP32 activations (A = float[M][K]) x Q4_0 / Q8_0 weights, fp32 arithmetic.

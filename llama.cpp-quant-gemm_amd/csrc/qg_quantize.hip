@@ -189,6 +189,74 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
     }
 }
 
+// Q8_1, eight lanes per block (round 5): the one-thread-per-block kernel above ran a
+// decode-size activation row (K = 4096: 128 blocks) as ONE workgroup whose 128 threads each walked 32
+// elements through ~350 dependent VALU ops — 4.4-5.5 us for 16 KB (profiles/r04c_bench_kernel_trace*.md).
+// Here lane j of a block's 8 lanes loads elements 4j..4j+3 (one 16-B load per lane, 1 KB contiguous per
+// wave instruction), 64-thread workgroups (8 blocks each: 16 workgroups at K = 4096) spread the row over
+// the CUs, and the per-lane work is 4 elements. Bytes identical to quantize_q8_1_block /
+// quantize_q8_1_block_def:
+//   amax: max over the 8 lanes' partial maxima (v_max_f32 is order-free on non-NaN values; every partial
+//     starts at 0.0f as the sequential loop does, so NaN inputs are ignored the same way);
+//   s = sum(x) in ELEMENT order: the partial sum walks the 8 lanes in turn (lane j adds its 4 elements to
+//     what lane j - 1 handed over by DPP row_shr:1), the very sequence of fp32 adds of the reference loop;
+//   variant 1: s = d * sum(q) (an integer sum, any order).
+// Lane j stores qs dword j; lane 7 (which ends holding s) stores the d | s dword.
+template <int VARIANT>
+__global__ __launch_bounds__(64) void quantize_q8_1_lanes_kernel(const float4* __restrict__ x, uint32_t* __restrict__ y,
+                                                                 int64_t nblocks) {
+    const int64_t gi = (int64_t)blockIdx.x * 64 + threadIdx.x;  // float4 index: block gi / 8, lane j = gi % 8
+    const int64_t ib = gi >> 3;
+    const int j = threadIdx.x & 7;
+    const bool ok = ib < nblocks;
+    const float4 v = ok ? x[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float m = fmaxf(fmaxf(fmaxf(fmaxf(0.0f, fabsf(v.x)), fabsf(v.y)), fabsf(v.z)), fabsf(v.w));
+    m = fmaxf(m, dpp_f<0xB1>(m));   // quad_perm [1,0,3,2]
+    m = fmaxf(m, dpp_f<0x4E>(m));   // quad_perm [2,3,0,1]
+    m = fmaxf(m, dpp_f<0x141>(m));  // row_half_mirror: the other quad of the 8 lanes
+    const float xs[4] = {v.x, v.y, v.z, v.w};
+    uint32_t qd = 0;
+    int sq = 0;
+    float d;
+    if constexpr (VARIANT == 2) {
+        d = m > 0.0f ? m / 127.0f : 1.0f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float r = fminf(fmaxf(rintf(xs[e] / d), -128.0f), 127.0f);
+            qd |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
+        }
+    } else {
+        d = m / 127.0f;
+        const float id = d > 0.0f ? 1.0f / d : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            int t = (int)roundf(xs[e] * id);
+            t = VARIANT == 1 ? max(-127, min(127, t)) : max(-128, min(127, t));
+            sq += t;
+            qd |= ((uint32_t)t & 0xFFu) << (8 * e);
+        }
+    }
+    float s;
+    if constexpr (VARIANT == 1) {
+        sq += __builtin_amdgcn_update_dpp(0, sq, 0xB1, 0xF, 0xF, false);
+        sq += __builtin_amdgcn_update_dpp(0, sq, 0x4E, 0xF, 0xF, false);
+        sq += __builtin_amdgcn_update_dpp(0, sq, 0x141, 0xF, 0xF, false);
+        s = (float)sq * d;
+    } else {
+        float p = 0.0f;
+#pragma unroll
+        for (int step = 0; step < 8; ++step) {
+            if (j == step) p = (((p + v.x) + v.y) + v.z) + v.w;
+            if (step < 7) p = dpp_f<0x111>(p);  // row_shr:1: lane step + 1 takes the running sum
+        }
+        s = p;  // complete in lane 7
+    }
+    if (!ok) return;
+    uint32_t* dst = y + ib * 9;
+    dst[1 + j] = qd;
+    if (j == 7) dst[0] = f2h_bits(d) | (f2h_bits(s) << 16);
+}
+
 // FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143), the
 // workspace producer of qg_gemm_q4_0_fp16_fused_ws for token counts beyond the fused GEMV.
 __global__ __launch_bounds__(256) void quantize_f16_fused_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ y,
@@ -277,6 +345,13 @@ hipError_t launch_quantize_q8_1_padded(const float* x, void* y, int64_t rows, in
 namespace {
 template <int TYPE, int VARIANT>
 hipError_t lq(const float* x, void* y, int64_t nblocks, hipStream_t st) {
+    if constexpr (TYPE == FMT_Q8_1) {
+        if (((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 3) == 0 && (nblocks + 7) / 8 <= 0x7fffffffL) {
+            hipLaunchKernelGGL((quantize_q8_1_lanes_kernel<VARIANT>), dim3((unsigned)((nblocks + 7) / 8)), dim3(64), 0, st,
+                               (const float4*)x, (uint32_t*)y, nblocks);
+            return hipGetLastError();
+        }
+    }
     const dim3 grid((unsigned)((nblocks + 255) / 256));
     if (((uintptr_t)x & 15) == 0)
         hipLaunchKernelGGL((quantize_kernel<TYPE, VARIANT, true>), grid, dim3(256), 0, st, x, (uint8_t*)y, nblocks);

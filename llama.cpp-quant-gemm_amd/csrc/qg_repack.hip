@@ -11,6 +11,7 @@
 // runs the same MFMA instantiation into a [M][N][K'/32] image and compacts it to [M][N][K/32].
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
+#include "qg_mmq_kernel.hpp"  // tiled_fmt: the LAY_TILED planes
 
 namespace qg {
 
@@ -57,6 +58,43 @@ __global__ __launch_bounds__(256) void repack_pad_kernel(const uint16_t* __restr
             if (off + 2 * h < sb) v |= (uint64_t)s[h] << (16 * h);
     }
     dst[i] = v;
+}
+
+// LAY_TILED (qg_tile_weights; the layout is specified with tiled_fmt in qg_mmq_kernel.hpp): one thread per
+// block slot (row r of the tile-padded N, block b of the stage-padded K/32) reads its source block (2-B
+// aligned: u16 loads; zero bytes for r >= N or b >= nb) and scatters its fields into the planes of its
+// (tile, stage) run. A load-time copy: the scattered 4-B stores are not on any per-call path.
+template <int F>
+__global__ __launch_bounds__(256) void tile_weights_kernel(const uint16_t* __restrict__ B, uint8_t* __restrict__ Bt, int N, int nb,
+                                                          int H, long total) {
+    using T = wfmt<F>;
+    using TF = tiled_fmt<F>;
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int nbp = H * MMQ_SB;
+    const long r = g / nbp;
+    const int b = (int)(g - r * nbp);
+    constexpr int HW = T::BB / 2;  // u16 words per block
+    uint16_t w[HW];
+#pragma unroll
+    for (int i = 0; i < HW; ++i) w[i] = 0;
+    if (r < N && b < nb) {
+        const uint16_t* src = B + (r * nb + b) * HW;
+#pragma unroll
+        for (int i = 0; i < HW; ++i) w[i] = src[i];
+    }
+    auto dw = [&](int byte_off) { return (uint32_t)w[byte_off / 2] | ((uint32_t)w[byte_off / 2 + 1] << 16); };
+    const int rr = (int)(r % TILE_ROWS), i16 = rr / 16, r16 = rr % 16, h = b / MMQ_SB, bb = b % MMQ_SB;
+    uint8_t* st = Bt + ((r / TILE_ROWS) * H + h) * (long)TF::STG;
+    constexpr int NQ = T::Q8 ? 8 : 4;  // qs dwords per block
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        const int qq = j % 4, half = j / 4;
+        *reinterpret_cast<uint32_t*>(st + i16 * 64 * TF::QSL + half * 1024 + (qq * 16 + r16) * 16 + bb * 4) = dw(T::QS + 4 * j);
+    }
+    if constexpr (T::QH >= 0) *reinterpret_cast<uint32_t*>(st + TF::OQH + rr * 16 + bb * 4) = dw(T::QH);
+    *reinterpret_cast<uint16_t*>(st + TF::OSC + rr * TF::SCB + bb * 2) = w[0];
+    if constexpr (T::MOFF >= 0) *reinterpret_cast<uint16_t*>(st + TF::OSC + rr * TF::SCB + 8 + bb * 2) = w[T::MOFF / 2];
 }
 
 // sumi image [M][N][nbp] -> [M][N][nb]
@@ -109,6 +147,30 @@ hipError_t launch_pad_rows(const void* src, void* dst, long rows, int rb, int rb
     hipLaunchKernelGGL(repack_pad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<const uint16_t*>(src),
                        static_cast<uint64_t*>(dst), words, rb, rbp, static_cast<const uint16_t*>(nullptr),
                        static_cast<uint64_t*>(nullptr), 0L, 0, 8);
+    return hipGetLastError();
+}
+
+size_t tiled_weight_bytes(int N, int K, int wtype) {
+    const long tiles = (N + TILE_ROWS - 1) / TILE_ROWS, stages = (K / QK + MMQ_SB - 1) / MMQ_SB;
+    return (size_t)(tiles * stages * TILE_ROWS * MMQ_SB * wbytes(wtype));
+}
+
+hipError_t launch_tile_weights(const void* B, void* Bt, int N, int K, int wtype, hipStream_t st) {
+    const int nb = K / QK, H = (nb + MMQ_SB - 1) / MMQ_SB;
+    const long total = (long)(N + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS * H * MMQ_SB;
+    const long blocks = (total + 255) / 256;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
+    const uint16_t* b16 = static_cast<const uint16_t*>(B);
+    uint8_t* bt = static_cast<uint8_t*>(Bt);
+    switch (wtype) {
+        case FMT_Q4_0: hipLaunchKernelGGL(tile_weights_kernel<FMT_Q4_0>, dim3((unsigned)blocks), dim3(256), 0, st, b16, bt, N, nb, H, total); break;
+        case FMT_Q4_1: hipLaunchKernelGGL(tile_weights_kernel<FMT_Q4_1>, dim3((unsigned)blocks), dim3(256), 0, st, b16, bt, N, nb, H, total); break;
+        case FMT_Q5_0: hipLaunchKernelGGL(tile_weights_kernel<FMT_Q5_0>, dim3((unsigned)blocks), dim3(256), 0, st, b16, bt, N, nb, H, total); break;
+        case FMT_Q5_1: hipLaunchKernelGGL(tile_weights_kernel<FMT_Q5_1>, dim3((unsigned)blocks), dim3(256), 0, st, b16, bt, N, nb, H, total); break;
+        case FMT_Q8_0: hipLaunchKernelGGL(tile_weights_kernel<FMT_Q8_0>, dim3((unsigned)blocks), dim3(256), 0, st, b16, bt, N, nb, H, total); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -237,6 +237,41 @@ def gemm_w4a8_prepacked(activation_q: torch.Tensor, weight_packed: torch.Tensor,
     return out
 
 
+def tile_weights(weight_q: torch.Tensor, N: int, K: int, wtype: int = Q4_0) -> torch.Tensor:
+    """Load-time tiled layout (qg_tile_weights): 1-D uint8 of qg_tile_weights_bytes(N, K, wtype) —
+    rows in tiles of 32, K/32 in stages of 4 blocks, each (tile, stage) one contiguous run in the
+    prefill kernel's operand order. Feed it to gemm_w4a8_tiled."""
+    _require(weight_q.is_cuda and weight_q.dtype == torch.uint8, "weight_q must be a CUDA uint8 tensor")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(weight_q.numel() == N * (K // 32) * BLOCK_BYTES[wtype], "Weight shape mismatch")
+    lib = _lib.load()
+    out = torch.empty(lib.qg_tile_weights_bytes(N, K, wtype), dtype=torch.uint8, device=weight_q.device)
+    w = weight_q.contiguous()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.qg_tile_weights(_ptr(w), _ptr(out), N, K, wtype, _stream(w.device)), "tile_weights")
+    return out
+
+
+def gemm_w4a8_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: int, N: int, K: int,
+                    wtype: int = Q4_0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C [M, N] = the same product as gemm_w4a8(activation_q, weight_q, ...) from
+    tile_weights(weight_q) (qg_gemm_w4a8_tiled; any K % 32 == 0)."""
+    _require(activation_q.is_cuda and weight_tiled.is_cuda, "Inputs must be CUDA tensors")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(activation_q.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    lib = _lib.load()
+    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    a = activation_q.contiguous()
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    _require(out.is_cuda and out.dtype == torch.float32 and out.shape == (M, N) and out.is_contiguous(),
+             "out must be a contiguous CUDA float32 [M, N] tensor")
+    with torch.cuda.device(a.device):
+        _lib.check(lib.qg_gemm_w4a8_tiled(_ptr(a), _ptr(weight_tiled), _ptr(out), M, N, K, wtype, _stream(a.device)),
+                   "gemm_w4a8_tiled")
+    return out
+
+
 def quantize_q8_1_padded(x: torch.Tensor) -> torch.Tensor:
     """x float32 [M, K] -> uint8 [M, K'/32, 36] (qg_quantize_q8_1_padded): each row's blocks as
     quantize_q8_1, then zero blocks up to K'/32 = round_up(K/32, 8) — the activation side of the
@@ -426,6 +461,26 @@ def debug_config(M: int, N: int, K: int, wtype: int = Q4_0, algo: int = ALGO_AUT
     return buf.value.decode()
 
 
+def debug_sumi_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: int, N: int, K: int,
+                     wtype: int = Q4_0) -> torch.Tensor:
+    """Per-block int32 dots [M, N, K/32] from the instantiation gemm_w4a8_tiled launches."""
+    _check_blocks(activation_q, "Activation", M, K, 36)
+    lib = _lib.load()
+    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    out = torch.empty((M, N, K // 32), dtype=torch.int32, device=weight_tiled.device)
+    with torch.cuda.device(weight_tiled.device):
+        _lib.check(lib.qg_debug_sumi_tiled(_ptr(activation_q.contiguous()), _ptr(weight_tiled), _ptr(out), M, N, K, wtype,
+                                           _stream(weight_tiled.device)), "debug_sumi_tiled")
+    return out
+
+
+def debug_config_tiled(M: int, N: int, K: int, wtype: int = Q4_0, sumi: bool = False) -> str:
+    """The instantiation gemm_w4a8_tiled (or debug_sumi_tiled with sumi=True) launches; nothing runs."""
+    buf = ctypes.create_string_buffer(256)
+    _lib.check(_lib.load().qg_debug_config_tiled(M, N, K, wtype, int(sumi), buf, 256), "debug_config_tiled")
+    return buf.value.decode()
+
+
 def select_algo(M: int, N: int, K: int, wtype: int = Q4_0) -> int:
     return _lib.load().qg_select_algo(M, N, K, wtype)
 
@@ -443,5 +498,6 @@ __all__ = [
     "gemm_w4a8_batched", "debug_sumi", "debug_config", "select_algo", "version",
     "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused", "gemm_w8a8", "gemm_q8_0_q8_1",
     "gemm_w4a16", "gemm_w8a16", "gemm_q4_0_fp32",
+    "tile_weights", "gemm_w4a8_tiled", "debug_sumi_tiled", "debug_config_tiled",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

@@ -37,6 +37,12 @@ SIGNATURES = {
     "qg_gemm_w4a8_prepacked_workspace_size": ([I, I], SZ),
     "qg_gemm_w4a8_prepacked": ([P, P, P, I, I, I, I, P, SZ, P], I),
     "qg_quantize_q8_1_padded": ([P, P, I, I, P], I),
+    "qg_tile_weights_bytes": ([I, I, I], SZ),
+    "qg_tile_weights": ([P, P, I, I, I, P], I),
+    "qg_gemm_w4a8_tiled": ([P, P, P, I, I, I, I, P], I),
+    "qg_gemm_w4a8_tiled_ldc": ([P, P, P, I, I, I, I64, I, P], I),
+    "qg_debug_sumi_tiled": ([P, P, P, I, I, I, I, P], I),
+    "qg_debug_config_tiled": ([I, I, I, I, I, ctypes.c_char_p, SZ], I),
     "qg_gemm_w4a8_padded": ([P, P, P, I, I, I, I, P], I),
     "qg_gemm_q4_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),

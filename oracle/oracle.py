@@ -276,6 +276,38 @@ def nmse(out: np.ndarray, ref: np.ndarray) -> float:
     return num / den if den > 0 else (0.0 if num == 0 else float("inf"))
 
 
+def tile_weights(b_q: np.ndarray, t: int) -> np.ndarray:
+    """numpy restatement of the tiled weight layout (qg_tile_weights; the device layout is specified
+    by tiled_fmt in llama.cpp-quant-gemm_amd/csrc/qg_mmq_kernel.hpp): [N, K/32, BB] block bytes ->
+    1-D bytes, rows in tiles of 32, K/32 in stages of 4 blocks, each (tile, stage) one run of
+    128 * BB bytes holding the planes
+      QS [row tile i (16 rows)][half][q][r][block][4 B]: qs dword q (+ 4 * half: Q8_0) of row 16 i + r,
+      QH [row][block][4 B] (Q5_0 / Q5_1), SC [row][d of blocks 0..3][m of blocks 0..3 (Q4_1 / Q5_1)],
+    zero bytes for rows past N and blocks past K/32. A layout check for the tests; not an oracle of
+    the reference (the reference has no tiled layout)."""
+    n, nb, bb = b_q.shape
+    assert bb == BLOCK_BYTES[t]
+    tiles, stages = -(-n // 32), -(-nb // 4)
+    full = np.zeros((tiles * 32, stages * 4, bb), np.uint8)
+    full[:n, :nb] = b_q
+    blk = full.reshape(tiles, 32, stages, 4, bb).transpose(0, 2, 1, 3, 4)  # [tile][stage][row][block][byte]
+    qs_off = {Q4_0: 2, Q4_1: 4, Q5_0: 6, Q5_1: 8, Q8_0: 2}[t]
+    nq = 8 if t == Q8_0 else 4
+    qs = blk[..., qs_off:qs_off + 4 * nq].reshape(tiles, stages, 2, 16, 4, nq // 4, 4, 4)  # i r b half q byte
+    qs = qs.transpose(0, 1, 2, 5, 6, 3, 4, 7)  # [tile][stage][i][half][q][r][block][byte]
+    parts = [qs.reshape(tiles, stages, -1)]
+    if t in (Q5_0, Q5_1):
+        qh_off = 2 if t == Q5_0 else 4
+        parts.append(blk[..., qh_off:qh_off + 4].reshape(tiles, stages, -1))
+    sc = [blk[..., 0:2]]
+    if t in (Q4_1, Q5_1):
+        sc.append(blk[..., 2:4])
+    parts.append(np.concatenate([x.reshape(tiles, stages, 32, 8) for x in sc], axis=-1).reshape(tiles, stages, -1))
+    out = np.concatenate(parts, axis=-1)
+    assert out.shape[-1] == 128 * bb
+    return np.ascontiguousarray(out).reshape(-1)
+
+
 def _h(x: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(x).view(np.float16).astype(np.float32)[..., 0]
 

@@ -182,7 +182,9 @@ def test_headline_configs_kernels(lib):
     assert qg.debug_config(1, 4096, 4096, 2).startswith("gemv F=2 MT=1 BPL=2 LPR=64 WGS=1024")
     assert "ONEU=1" in qg.debug_config(1, 4096, 4096, 2)
     assert qg.debug_config(32, 4096, 4096, 2).startswith("mmq F=2 ")
-    assert "EPI2=1" in qg.debug_config(32, 4096, 4096, 2)
+    assert "BN=32 TT=1 W=12 P16=1 NB=1 LAY=0 AW=0" in qg.debug_config(32, 4096, 4096, 2)
+    # the tiled layout of the same config: same tile, same waves
+    assert "BN=32 TT=1 W=12 P16=1 NB=1 LAY=1 AW=0" in qg.debug_config_tiled(32, 4096, 4096, 2)
     for t in (3, 6, 7):
         assert qg.debug_config(1, 4096, 4096, t).startswith(f"gemv F={t} MT=1 ")
     assert qg.debug_config(1, 4000, 4096, 2).startswith("gemv F=2 MT=1 ")

@@ -53,8 +53,10 @@ def test_prepacked_workspace_contract(qg):
     b = torch.zeros(16 * 136 * 18, dtype=torch.uint8, device="cuda")
     c = torch.zeros(32 * 16, dtype=torch.float32, device="cuda")
     P = ctypes.c_void_p
-    # K' != K without a workspace: refused, nothing launched
-    assert lib.qg_gemm_w4a8_prepacked(P(a.data_ptr()), P(b.data_ptr()), P(c.data_ptr()), 32, 16, 4128, 2, None, 0, st) == -1
+    # K' != K without a workspace: refused on the GEMV path (M <= 4), nothing launched; the MFMA path
+    # (M >= 5) reads the plain activation rows itself since round 5 and needs none
+    assert lib.qg_gemm_w4a8_prepacked(P(a.data_ptr()), P(b.data_ptr()), P(c.data_ptr()), 3, 16, 4128, 2, None, 0, st) == -1
+    assert lib.qg_gemm_w4a8_prepacked(P(a.data_ptr()), P(b.data_ptr()), P(c.data_ptr()), 32, 16, 4128, 2, None, 0, st) == 0
 
 
 @pytest.mark.parametrize("t", [2, 8])

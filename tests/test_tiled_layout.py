@@ -1,0 +1,66 @@
+"""The tiled weight layout's restatement (oracle.tile_weights) against its per-block placement formula
+(CPU only). The device layout is specified once, by tiled_fmt in
+llama.cpp-quant-gemm_amd/csrc/qg_mmq_kernel.hpp; here each block's fields are placed one by one with
+those offsets (a pure-Python loop, the formula qg_tile_weights' kernel implements) and the vectorised
+restatement the GPU tests compare against must agree byte for byte. Also: the layout is a bijection on
+the real bytes (every source byte lands exactly once, everything else is zero padding)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+QS = {2: 2, 3: 4, 6: 6, 7: 8, 8: 2}
+QH = {6: 2, 7: 4}
+MOFF = {3: 2, 7: 2}
+
+
+def place_loop(bq, t):
+    n, nb, bb = bq.shape
+    tiles, stages = -(-n // 32), -(-nb // 4)
+    q8 = t == 8
+    qsl = 32 if q8 else 16
+    qhb = 16 if t in QH else 0
+    scb = 16 if t in MOFF else 8
+    oqh, osc = 2 * 64 * qsl, 2 * 64 * qsl + 32 * qhb
+    stg = osc + 32 * scb
+    assert stg == 128 * bb
+    out = np.zeros(tiles * stages * stg, np.uint8)
+    for r in range(tiles * 32):
+        for b in range(stages * 4):
+            blk = bq[r, b] if r < n and b < nb else np.zeros(bb, np.uint8)
+            rr, h, bb4 = r % 32, b // 4, b % 4
+            base = ((r // 32) * stages + h) * stg
+            for j in range(8 if q8 else 4):
+                q, half = j % 4, j // 4
+                o = base + (rr // 16) * 64 * qsl + half * 1024 + (q * 16 + rr % 16) * 16 + bb4 * 4
+                out[o:o + 4] = blk[QS[t] + 4 * j:QS[t] + 4 * j + 4]
+            if t in QH:
+                o = base + oqh + rr * 16 + bb4 * 4
+                out[o:o + 4] = blk[QH[t]:QH[t] + 4]
+            o = base + osc + rr * scb + bb4 * 2
+            out[o:o + 2] = blk[0:2]
+            if t in MOFF:
+                out[o + 8:o + 10] = blk[MOFF[t]:MOFF[t] + 2]
+    return out
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+@pytest.mark.parametrize("n,nb", [(32, 4), (37, 9), (5, 1), (70, 13)])
+def test_tile_weights_restatement_matches_placement(t, n, nb):
+    rng = np.random.default_rng(n * 31 + nb + t)
+    bq = rng.integers(0, 256, (n, nb, O.BLOCK_BYTES[t]), dtype=np.uint8)
+    fast = O.tile_weights(bq, t)
+    assert np.array_equal(fast, place_loop(bq, t))
+
+
+@pytest.mark.parametrize("t", [2, 3, 6, 7, 8])
+def test_tile_weights_is_a_permutation_of_the_real_bytes(t):
+    """Byte multiset: tiling distinct byte ids (as uint16 positions in a 2-byte encoding) keeps every
+    source byte exactly once."""
+    n, nb = 45, 11
+    bb = O.BLOCK_BYTES[t]
+    ids = np.arange(n * nb * bb, dtype=np.int64)
+    lo = (ids % 251 + 1).astype(np.uint8).reshape(n, nb, bb)  # nonzero marker bytes
+    tiled = O.tile_weights(lo, t)
+    assert np.count_nonzero(tiled) == n * nb * bb
+    assert np.array_equal(np.sort(tiled[tiled != 0]), np.sort(lo.reshape(-1)))
