@@ -87,88 +87,145 @@ def graph_time_us(fn, reps: int = 10, per: int = 1) -> float:
     return e0.elapsed_time(e1) * 1e3 / (reps * per)
 
 
+# The reference's published per-shape numbers (RTX 5070 Laptop; weight-major rows x tokens x K in its
+# reports, here activation-major M tokens, N weight rows): BASELINE.md §1.
+REF_PUBLISHED = {
+    (1, 4096, 4096): (622.3, "docs/2d_tiling_final_report.md:70"),
+    (1, 4096, 14336): (594.5, "docs/2d_tiling_final_report.md:71"),
+    (2, 4096, 14336): (610.4, "docs/2d_tiling_final_report.md:72"),
+    (4, 4096, 14336): (623.4, "docs/2d_tiling_final_report.md:73"),
+    (2, 8192, 14336): (630.4, "docs/2d_tiling_final_report.md:74"),
+    (512, 4096, 4096): (2700.0, "README.md:827-830 (tiled+dp4a, ~2.7 TFLOPS)"),
+}
+I8_DENSE_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: dense int8/fp8 MFMA ~5 P(FL)OPS (no sparsity)
+
+
+def load_pmc(cfg_key: str, field: str):
+    """A per-config PMC figure recorded by a rocprofv3 --pmc pass (profiles/*pmc*.json), if present."""
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir), reverse=True):
+        if f.endswith(".json") and "pmc" in f:
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except (OSError, ValueError):
+                continue
+            v = d.get(cfg_key, {}).get(field)
+            if v is not None:
+                return {"value": v, "source": f"profiles/{f}"}
+    return None
+
+
 def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: int = 10,
-                   forms: tuple = ("single",)) -> list:
+                   forms: tuple = ("single",), label: str = "") -> list:
     """A BASELINE side config on this GPU the way the headline is measured: step4-recipe data,
     G launches of the product dispatch (qg_gemm_w4a8, auto) over rotating resident weight copies
     (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays.
     forms: "single" (G launches), "batched" (one qg_gemm_w4a8_grouped launch over the G copies),
-    "prepacked" / "padded" (the load-time padded layout), "w16" (qg_gemm_w4a16_ws: FP32 activations)."""
+    "prepacked" / "padded" (the load-time padded layout), "tiled" (the load-time tiled layout,
+    qg_tile_weights + qg_gemm_w4a8_tiled), "w16" (qg_gemm_w4a16_ws: FP32 activations). Every row
+    carries the NMSE vs an fp64 product of the unquantized inputs of ITS OWN form's output."""
     wt = WTYPES[wname]
     bb = qg.BLOCK_BYTES[wt]
     a_h, b_h = qhost.fill_step4(M, N, K, 42, 0, N)
     a, b = torch.from_numpy(a_h).to(dev), torch.from_numpy(b_h).to(dev)
     del a_h, b_h
     aq, bq = qg.quantize_q8_1(a), qg.quantize(b, wt)
-    c = qg.gemm_w4a8(aq, bq, M, N, K, wt)
     ref = a.double() @ b.double().T
-    nmse = float(torch.sum((c.double() - ref) ** 2) / torch.sum(ref ** 2))
+    den = torch.sum(ref ** 2)
+    nmse_of = lambda c: float(torch.sum((c.double() - ref) ** 2) / den)
     af = a if "w16" in forms else None  # W4A16: the FP32 activations themselves
-    if af is not None:
-        c16 = qg.gemm_w4a16(af, bq, M, N, K)
-        nmse16 = float(torch.sum((c16.double() - ref) ** 2) / torch.sum(ref ** 2))
-        del c16
-    del a, b, ref, c
-    if "prepacked" in forms or "padded" in forms:  # the load-time layout for K/32 % 8 != 0 (qg_repack_weights)
-        bq = qg.repack_weights(bq, N, K, wt)
-        ap = qg.quantize_q8_1_padded(torch.from_numpy(qhost.fill_step4(M, N, K, 42, 0, 0)[0]).to(dev))
-    R = max(G, math.ceil(600e6 / bq.numel()))
-    copies = torch.empty((R,) + tuple(bq.shape), dtype=torch.uint8, device=dev)
-    copies.copy_(bq.unsqueeze(0).expand_as(copies))
-    out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+    ap = None
+    if "padded" in forms:
+        ap = qg.quantize_q8_1_padded(a)
+    del b
     nbytes = algo_bytes(M, N, K, bb)
     res = []
+    lib = qg._lib.load()
+    variant_of = {"prepacked": "repacked", "padded": "repacked", "tiled": "tiled"}
+    copies, cur = None, None
     for form in forms:
+        var = variant_of.get(form, "rows")
+        if var != cur:
+            del copies
+            torch.cuda.empty_cache()
+            w = bq if var == "rows" else qg.repack_weights(bq, N, K, wt) if var == "repacked" else qg.tile_weights(bq, N, K, wt)
+            R = max(G, math.ceil(600e6 / w.numel()))
+            copies = torch.empty((R,) + tuple(w.shape), dtype=torch.uint8, device=dev)
+            copies.copy_(w.unsqueeze(0).expand_as(copies))
+            cur = var
+            del w
+        out = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+        P = ctypes.c_void_p
         if form == "single":
             def step() -> None:
                 for j in range(G):
                     qg.gemm_w4a8(aq, copies[j], M, N, K, wt, out=out[j])
+        elif form == "tiled":
+            def step() -> None:
+                cs = P(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_gemm_w4a8_tiled(P(aq.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N, K,
+                                              wt, cs) != 0:
+                        raise RuntimeError("qg_gemm_w4a8_tiled failed")
         elif form == "prepacked":
-            lib = qg._lib.load()
             wsb = lib.qg_gemm_w4a8_prepacked_workspace_size(M, K)
             ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
 
             def step() -> None:
-                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                cs = P(torch.cuda.current_stream().cuda_stream)
                 for j in range(G):
-                    if lib.qg_gemm_w4a8_prepacked(ctypes.c_void_p(aq.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
-                                                  ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt,
-                                                  ctypes.c_void_p(ws.data_ptr()), wsb, cs) != 0:
+                    if lib.qg_gemm_w4a8_prepacked(P(aq.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N, K,
+                                                  wt, P(ws.data_ptr()), wsb, cs) != 0:
                         raise RuntimeError("qg_gemm_w4a8_prepacked failed")
         elif form == "w16":  # qg_gemm_w4a16 with a caller workspace (the library's is never handed to a capture)
-            lib = qg._lib.load()
             wsb = lib.qg_gemm_w16_workspace_size(M, N, K)
             ws16 = torch.zeros(max(wsb, 16) // 4 + 64, dtype=torch.int32, device=dev)
 
             def step() -> None:
-                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                cs = P(torch.cuda.current_stream().cuda_stream)
                 for j in range(G):
-                    if lib.qg_gemm_w4a16_ws(ctypes.c_void_p(af.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
-                                            ctypes.c_void_p(out[j].data_ptr()), M, N, K, ctypes.c_void_p(ws16.data_ptr()),
-                                            wsb, cs) != 0:
+                    if lib.qg_gemm_w4a16_ws(P(af.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N, K,
+                                            P(ws16.data_ptr()), wsb, cs) != 0:
                         raise RuntimeError("qg_gemm_w4a16_ws failed")
         elif form == "padded":
-            lib = qg._lib.load()
-
             def step() -> None:
-                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                cs = P(torch.cuda.current_stream().cuda_stream)
                 for j in range(G):
-                    if lib.qg_gemm_w4a8_padded(ctypes.c_void_p(ap.data_ptr()), ctypes.c_void_p(copies[j].data_ptr()),
-                                               ctypes.c_void_p(out[j].data_ptr()), M, N, K, wt, cs) != 0:
+                    if lib.qg_gemm_w4a8_padded(P(ap.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N, K, wt,
+                                               cs) != 0:
                         raise RuntimeError("qg_gemm_w4a8_padded failed")
         else:
             def step() -> None:
                 qg.gemm_w4a8_grouped([aq] * G, [copies[j] for j in range(G)], [N] * G, M, K, wt,
                                      outs=[out[j] for j in range(G)])
         us = graph_time_us(step, reps, G)
+        nmse = nmse_of(out[0])  # this form's own output of the timed launches
         fb = nbytes if form != "w16" else nbytes + M * K * 4 - M * (K // 32) * 36  # FP32 activations
-        res.append({"wtype": wname if form != "w16" else wname + "_fp32_w4a16", "M": M, "N": N, "K": K, "form": form,
-                    "kernel_algo": int(qg.select_algo(M, N, K, wt)) if form != "w16" else None,
-                    "us_per_launch" if form in ("single", "prepacked", "padded", "w16") else "us_per_gemv": round(us, 3),
-                    "gbps": round(fb / us / 1e3, 1),
-                    "frac_hbm": round(fb / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(2.0 * M * N * K / us / 1e6, 2),
-                    "nmse_vs_fp32": nmse if form != "w16" else nmse16})
-    del copies, out
+        tops = 2.0 * M * N * K / us / 1e6
+        row = {"wtype": wname if form != "w16" else wname + "_fp32_w4a16", "M": M, "N": N, "K": K, "form": form,
+               "kernel_algo": int(qg.select_algo(M, N, K, wt)) if form in ("single", "batched") else None,
+               "us_per_launch" if form != "batched" else "us_per_gemv": round(us, 3),
+               "gbps": round(fb / us / 1e3, 1),
+               "frac_hbm": round(fb / us / 1e3 / HBM_PEAK_GBPS, 4), "tops": round(tops, 2),
+               "nmse_vs_fp32": nmse}
+        if label:
+            row["label"] = label
+        pub = REF_PUBLISHED.get((M, N, K))
+        if pub and form in ("single", "tiled") and wname == "q4_0":
+            row["ref_published_gflops"], row["ref_source"] = pub
+            row["vs_ref_published"] = round(tops * 1e3 / pub[0], 2)
+        if M >= 128 and form != "w16":
+            cfg = f"{wname}_m{M}_n{N}_k{K}" + ("_tiled" if form == "tiled" else "")
+            row["mfma"] = {"frac_dense_i8_peak": round(tops / I8_DENSE_PEAK_TOPS, 4), "peak_tops": I8_DENSE_PEAK_TOPS,
+                           "busy": load_pmc(cfg, "mfma_busy_frac"),
+                           "note": "busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles) from a recorded --pmc pass "
+                                   "of the same kernel (tools/profile_mfma.sh); frac = effective TOPS / dense i8 peak"}
+        res.append(row)
+        del out
+    del copies, ref
+    torch.cuda.empty_cache()
     return res
 
 
@@ -856,14 +913,31 @@ def main() -> None:
             # of G: the denominators of the N>1 strong-scaling ratios
             del mods, wcopies
             torch.cuda.empty_cache()
-            sides = [("q4_0", 32, 4096, 4096, ("single",)), ("q4_1", 1, 4096, 4096, ("single",)),
-                     ("q5_0", 1, 4096, 4096, ("single",)), ("q5_1", 1, 4096, 4096, ("single",)),
-                     ("q4_0", 1, 32000, 4096, ("single", "batched")),
-                     # odd K/32 at a prefill size from the load-time padded layout
-                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded")),
+            sides = [("q4_0", 32, 4096, 4096, ("single", "tiled"), "configs[2]"),
+                     ("q4_1", 1, 4096, 4096, ("single",), "configs[3]"),
+                     ("q5_0", 1, 4096, 4096, ("single",), "configs[3]"), ("q5_1", 1, 4096, 4096, ("single",), "configs[3]"),
+                     ("q4_0", 1, 32000, 4096, ("single", "batched"), "configs[4] on one GPU"),
+                     # odd K/32 at a prefill size: the load-time padded layout and the
+                     # tiled layout (round 5)
+                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded", "tiled"), "odd K/32"),
                      # row f3: the W4A16 prefill (FP32 activations x Q4_0), M = 32
-                     ("q4_0", 32, 4096, 4096, ("w16",))]
-            out["side_configs"] = [r for (w, m_, n_, k_, f) in sides for r in measure_config(w, m_, n_, k_, dev, forms=f)]
+                     ("q4_0", 32, 4096, 4096, ("w16",), "row f3"),
+                     # the reference's published shapes: 2D-tile table
+                     # (docs/2d_tiling_final_report.md:70-74, weight-major 4096/8192 x tokens x 14336), the
+                     # llama-shape batch-decode sweep (tests/test_llama_shapes.cu:6,256: 1..8 tokens at
+                     # 4096 x 14336) and the step4 prefill sizes (tests/step4_w4a8_gemm.cu:278-281)
+                     ("q4_0", 1, 4096, 14336, ("single",), "published 4096x1x14336"),
+                     ("q4_0", 2, 4096, 14336, ("single",), "published 4096x2x14336"),
+                     ("q4_0", 3, 4096, 14336, ("single",), "llama-shape sweep"),
+                     ("q4_0", 4, 4096, 14336, ("single",), "published 4096x4x14336"),
+                     ("q4_0", 5, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
+                     ("q4_0", 8, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
+                     ("q4_0", 2, 8192, 14336, ("single",), "published 8192x2x14336"),
+                     ("q4_0", 128, 4096, 4096, ("single", "tiled"), "step4 prefill"),
+                     ("q4_0", 512, 4096, 4096, ("single", "tiled"), "step4 prefill (published ~2.7 TFLOPS)"),
+                     ("q4_0", 512, 4096, 14336, ("single", "tiled"), "step4 prefill")]
+            out["side_configs"] = [r for (w, m_, n_, k_, f, lab) in sides
+                                   for r in measure_config(w, m_, n_, k_, dev, forms=f, label=lab)]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

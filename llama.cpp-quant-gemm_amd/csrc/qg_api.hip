@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -83,6 +84,24 @@ void* stream_workspace(hipStream_t st, size_t bytes, int slot, std::unique_lock<
     void* p = e->p;
     if (hold) *hold = std::move(lk);
     return p;
+}
+
+int device_cus() {
+    static std::atomic<int> cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return 256;
+    }
+    int v = cached[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+        (void)hipGetLastError();
+        cus = 256;
+    }
+    cached[dev].store(cus, std::memory_order_relaxed);
+    return cus;
 }
 
 void describe_kernel(const GemmArgs& g, const char* fmt, ...) {

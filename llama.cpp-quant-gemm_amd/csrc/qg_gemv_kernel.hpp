@@ -46,35 +46,6 @@
 
 namespace qg {
 
-#ifdef QG_STAMPS
-// diagnostic build only (tools/archive/timeline_probe.hip; never in the product build): per wave 8 slots: 100-MHz stamps at entry,
-// after the activation barrier, weights landed, compute done, exit; s_memtime at entry and exit;
-// (XCC_ID << 32 | HW_ID)
-__device__ unsigned long long g_stamps[8 * 65536];
-#define QG_STAMP(v) unsigned long long v = __builtin_amdgcn_s_memrealtime()
-#define QG_CLK(v) unsigned long long v = __builtin_amdgcn_s_memtime()
-#define QG_STAMP_STORE(...)                                                                       \
-    do {                                                                                          \
-        if ((threadIdx.x & 63) == 0) {                                                            \
-            unsigned hw, xcc;                                                                     \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));                      \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                    \
-            const int wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                   \
-            const unsigned long long vals[7] = {__VA_ARGS__};                                     \
-            for (int q = 0; q < 7; ++q) g_stamps[8 * wv + q] = vals[q];                           \
-            g_stamps[8 * wv + 7] = ((unsigned long long)xcc << 32) | hw;                          \
-        }                                                                                         \
-    } while (0)
-#define QG_WAIT_STAMP(v)                                                                          \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                              \
-    unsigned long long v = __builtin_amdgcn_s_memrealtime()
-#else
-#define QG_STAMP(v)
-#define QG_CLK(v)
-#define QG_STAMP_STORE(...)
-#define QG_WAIT_STAMP(v)
-#endif
-
 constexpr uint32_t ACC_BIAS = 0x4B400000u;  // bits of 12582912.0f = 1.5 * 2^23
 constexpr float ACC_BIAS_F = 12582912.0f;
 
@@ -220,11 +191,8 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // first 14 dwords, which the dispatch preloads into SGPRs (-amdgpu-kernarg-preload-count, Makefile);
 // the rest (output pointer and strides, the sumi hook) is fetched by an s_load that is only waited
 // for at the store, so no kernarg fetch sits in front of the weight stream.
-// ABL (tuning probes only; the product uses 0): bit 1 — no activation staging (records taken from a
-// constant: no A loads, no LDS, no barrier); bit 2 — no dot / epilogue (the weight dwords are summed);
-// bit 4 — nontemporal output stores; bit 8 — write-through (agent-scope, sc1) output stores;
-// bit 16 — M = 1: the workgroup's outputs gathered through LDS into one coalesced store.
-// bit 32 — output stores as agent-scope atomic exchanges (executed at the memory side: no dirty L2 lines).
+// (The round-1..4 ablation bits and timeline stamps used to decompose this kernel live in
+// tools/archive/qg_gemv_kernel_r04_knobs.hpp, not here.)
 // The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
 // minimal argument list.
 // TPW (tiles per workgroup, loop-free form only): the workgroup computes TPW consecutive row tiles of
@@ -232,14 +200,12 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int ABL, int TPW = 1>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
                                           int32_t* __restrict__ sumi_out, int tile_in = -1) {
-    static_assert(TPW == 1 || (ONEU && (ABL & ~32) == 0), "several tiles per workgroup: loop-free form only");
+    static_assert(TPW == 1 || ONEU, "several tiles per workgroup: loop-free form only");
     using G = gemv_geom<F, BPL>;
-    QG_STAMP(t0);
-    QG_CLK(c0);
     A = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A) + blockIdx.y * sA);
     B += blockIdx.y * sB;
     C += blockIdx.y * sC;
@@ -301,9 +267,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     // 1) activation block loads of this thread (one thread per block), the first before the
     //    weight stream; 2) the lane's first weight unit; 3) LDS records
     const int totb = M * nb;
-    if constexpr ((ABL & 1) != 0) {
-        load_first();
-    } else if constexpr (AIN == AIN_Q8_1) {
+    if constexpr (AIN == AIN_Q8_1) {
         uint32_t ab[9];
         auto load_ablk = [&](int g) {
             const uint32_t* p = A + (long)g * 9;
@@ -329,9 +293,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
             make_act_record<F>(w, lds + rec_of(g));
         }
     }
-    if constexpr ((ABL & 1) == 0) __syncthreads();
-    QG_STAMP(tb);
-    QG_WAIT_STAMP(t1);
+    __syncthreads();
 
     float acc[MT];
 #pragma unroll
@@ -347,10 +309,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
                 for (int m = 0; m < MT; ++m) {
                     const uint32_t* rec = lds + (min(m, M - 1) * U + u) * G::REC_DW + bi * 12;
 #pragma unroll
-                    for (int x = 0; x < 3; ++x) {
-                        if constexpr ((ABL & 1) != 0) pre[bi][m][x] = make_uint4(0x11u * (x + 1), 0x1234u, (uint32_t)u, 0x3F800000u);
-                        else pre[bi][m][x] = *reinterpret_cast<const uint4*>(rec + 4 * x);
-                    }
+                    for (int x = 0; x < 3; ++x) pre[bi][m][x] = *reinterpret_cast<const uint4*>(rec + 4 * x);
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -369,13 +328,6 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
                         a[0] = *reinterpret_cast<const uint4*>(rec);
                         a[1] = *reinterpret_cast<const uint4*>(rec + 4);
                         a[2] = *reinterpret_cast<const uint4*>(rec + 8);
-                    }
-                    if constexpr ((ABL & 2) != 0) {
-                        uint32_t x = a[2].w;
-#pragma unroll
-                        for (int v = 0; v < G::UDW; ++v) x += cur[v];
-                        acc[m] += __uint_as_float(x & 0x3FFFFFFFu);
-                        continue;
                     }
                     const uint32_t d = block_dot<F, bi>(cur, a);
                     if constexpr (SUMI) {
@@ -410,31 +362,13 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
             }
         }
     }
-    QG_STAMP(tc);
-    if constexpr (!SUMI && (ABL & 16) != 0 && MT == 1 && LPR == 64) {
-        // one coalesced store of the workgroup's RPB consecutive outputs (M = 1, unit stride)
-        __shared__ float obuf[WGS / 64];
-        acc[0] = group_sum_last<LPR>(acc[0]);
-        if (lane == 63) obuf[tid >> 6] = acc[0];
-        __syncthreads();
-        if (tid < RPB) {
-            const int r = tile * RPB + tid;
-            if (r < N) C[r] = obuf[tid];
-        }
-    } else if constexpr (!SUMI) {
+    if constexpr (!SUMI) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<LPR>(acc[m]);
         if (row_ok && lir == LPR - 1) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-                if (m < M) {
-                    if constexpr ((ABL & 4) != 0) __builtin_nontemporal_store(acc[m], C + m * ldc_m + row * ldc_n);
-                    else if constexpr ((ABL & 8) != 0)
-                        __hip_atomic_store(C + m * ldc_m + row * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    else if constexpr ((ABL & 32) != 0)
-                        (void)__hip_atomic_exchange(C + m * ldc_m + row * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    else C[m * ldc_m + row * ldc_n] = acc[m];
-                }
+                if (m < M) C[m * ldc_m + row * ldc_n] = acc[m];
         }
     }
     if constexpr (TPW > 1 && !SUMI) {
@@ -448,25 +382,18 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
             if (rows_ok[t] && lir == LPR - 1) {
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    if (m < M) {
-                        if constexpr ((ABL & 32) != 0)
-                            (void)__hip_atomic_exchange(C + m * ldc_m + rows[t] * ldc_n, acc[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        else C[m * ldc_m + rows[t] * ldc_n] = acc[m];
-                    }
+                    if (m < M) C[m * ldc_m + rows[t] * ldc_n] = acc[m];
             }
         }
     }
-    QG_STAMP(t2);
-    QG_CLK(c2);
-    QG_STAMP_STORE(t0, tb, t1, tc, t2, c0, c2);
 }
 
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
-          bool ONEU = false, int ABL = 0, int TPW = 1>
+          bool ONEU = false, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    long sA, long sB, int M, int N, int K, float* __restrict__ C,
                                                    long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
-    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, ONEU, ABL, TPW>(A, B, sA, sB, M, N, K, C, sC, ldc_m, ldc_n, sumi_out);
+    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, ONEU, TPW>(A, B, sA, sB, M, N, K, C, sC, ldc_m, ldc_n, sumi_out);
 }
 
 // M = 2..8, one product: (A, B, M, N, K, out, ldc_m, ldc_n) with 32-bit output strides = 10 dwords
@@ -474,7 +401,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool PRE = (MT <= 2), bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int M,
                                                     int N, int K, void* __restrict__ out, int ldc_m, int ldc_n) {
-    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, false, PRE, ONEU, 0>(A, B, 0, 0, M, N, K, SUMI ? nullptr : (float*)out, 0,
+    gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, false, PRE, ONEU>(A, B, 0, 0, M, N, K, SUMI ? nullptr : (float*)out, 0,
                                                                      ldc_m, ldc_n, SUMI ? (int32_t*)out : nullptr);
 }
 
@@ -483,16 +410,10 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
 // entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
-#ifndef QG_GEMV_WGSTORE
-#define QG_GEMV_WGSTORE 0
-#endif
-#ifndef QG_GEMV1_ABL
-#define QG_GEMV1_ABL 0  // (tuning A/B only) output-store ablation bits of the M = 1 entry, see gemv_body
-#endif
 template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
-    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, (QG_GEMV_WGSTORE ? 16 : 0) | QG_GEMV1_ABL>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 
@@ -557,7 +478,7 @@ __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     }
     const GemvItemDesc d = grp.it[item];
     if (tile * RPB >= d.N) return;  // past this item's rows (uniform)
-    gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, 0, TPW>(
+    gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, TPW>(
         reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K, d.C, 0,
         d.ldc, 1, nullptr, tile);
 }
@@ -638,7 +559,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                 const int rpw_full = one ? RPB * QG_GEMVG_TPW : RPB;
                 int nmax = 0;
                 for (int i = 0; i < grp0.count; ++i) nmax = std::max(nmax, grp0.it[i].N);
-                if ((nmax + rpw_full - 1) / rpw_full <= 256)
+                if ((nmax + rpw_full - 1) / rpw_full <= device_cus())
                     return go(std::integral_constant<int, GWH>{}, std::integral_constant<int, TPH>{});
             }
             return go(std::integral_constant<int, WGS>{}, std::integral_constant<int, QG_GEMVG_TPW>{});
@@ -681,8 +602,8 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     constexpr int TPB = MTB ? QG_GEMV_MTTPW : QG_GEMV_TPW;
     if constexpr (GWB < WGS && GWB >= 64 && !SUMI && !NT) {
         constexpr int GW = GWB, RPBB = (GW / 64) * (64 / LPR) * TPB;
-        if (one && g.batch > 1 && grid <= 256) {
-            auto kb = gemv_kernel<F, MT, BPL, LPR, GW, SUMI, AIN, NT, PRE, true, 0, TPB>;
+        if (one && g.batch > 1 && grid <= device_cus()) {
+            auto kb = gemv_kernel<F, MT, BPL, LPR, GW, SUMI, AIN, NT, PRE, true, TPB>;
             if (lds > 64 * 1024) {
                 hipError_t e = hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
@@ -694,7 +615,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     }
     constexpr bool tpw_ok = !SUMI && !NT && QG_GEMV_TPW > 1;
     const bool multi = tpw_ok && one && g.batch > 1;
-    auto kfn = multi ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true, 0, tpw_ok ? QG_GEMV_TPW : 1>
+    auto kfn = multi ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true, tpw_ok ? QG_GEMV_TPW : 1>
              : one   ? gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE, true>
                      : gemv_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, NT, PRE && (MT <= 2), false>;
     if (lds > 64 * 1024) {

@@ -67,6 +67,11 @@ inline hipError_t set_max_lds_once(const void* fn, int bytes, std::atomic<unsign
     return e;
 }
 
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount, cached per device; 256 on a
+// whole MI355X, and when no device is visible — the qg_debug_config queries of a GPU-less build host).
+// "One dispatch round" tile choices compare grids against it (CU-partitioned devices).
+int device_cus();
+
 // printf-style description of a kernel instantiation into g.describe (qg_debug_config). SUMI is
 // deliberately not part of it: the parity hook must name the product's kernel.
 void describe_kernel(const GemmArgs& g, const char* fmt, ...);

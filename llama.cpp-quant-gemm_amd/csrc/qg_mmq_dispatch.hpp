@@ -48,9 +48,9 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 template <int F, int BN, int TT> constexpr int alt_w = BN == 32 && TT == 1 ? 12 : BN == 16 ? (F != FMT_Q8_0 ? 16 : 8) : 8;
 template <int F, int BN, int TT> constexpr int alt_nb = BN == 32 && TT == 1 ? 1 : BN == 16 ? (F != FMT_Q8_0 ? 1 : 2) : 2;
 
-// grid of one dispatch round: one workgroup per CU
+// grid of one dispatch round: at most one workgroup per CU (device_cus(): 256 on a whole MI355X)
 inline bool one_round(const GemmArgs& g, int BN, int NTOK) {
-    return (long)((g.N + BN - 1) / BN) * ((g.M + NTOK - 1) / NTOK) <= 256;
+    return (long)((g.N + BN - 1) / BN) * ((g.M + NTOK - 1) / NTOK) <= device_cus();
 }
 
 template <int F, int BN, int TT, int W, bool P16, int LAY, bool AW> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
@@ -101,11 +101,11 @@ template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hi
     return hipErrorInvalidValue;
 }
 
-inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= 256; }
+inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 15) / 16) >= device_cus(); }
 
 // 8 waves per 32 x 32 tile only while that leaves <= 256 workgroups; beyond, 4-wave workgroups two
 // per CU (profiles/r01_tuning/mmq_probe_mid.txt: M=96 16.5 -> 14.2 us, M=128 17.3 -> 15.5 us)
-inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= 256; }
+inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= device_cus(); }
 }  // namespace mmqd
 
 // The configuration for the shape (above), or the 4-wave 32 x 32 tile where the preferred 8-wave one does

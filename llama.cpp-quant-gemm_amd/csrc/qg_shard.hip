@@ -69,6 +69,9 @@ int qg_sharded_gemm_w4a8_local(const void* A, const void* B_shard, float* C_slic
 
 int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, int N, int K, int wtype, void* ws,
                          size_t ws_bytes, qg_nccl_comm_t comm, qg_stream_t stream) {
+    // Arguments every rank passes alike (the communicator, the shape, the replicated activations and the
+    // output) are checked before anything is enqueued: on an error here EVERY rank returns before the
+    // collective, so none waits for the others.
     if (!comm) return QG_ERR_INVALID_ARG;
     if (M < 0 || N < 0) return QG_ERR_INVALID_ARG;
     if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
@@ -79,29 +82,39 @@ int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, in
     if (nccl_status(ncclCommUserRank((ncclComm_t)comm, &rank)) != QG_OK) return QG_ERR_HIP;
     int row0 = 0, rows = 0;
     qg_shard_rows(N, world, rank, &row0, &rows);
-    if (rows > 0 && !B_shard) return QG_ERR_INVALID_ARG;
     const long P = per_rank(N, world);
     const size_t count = (size_t)M * (size_t)P;
     hipStream_t st = (hipStream_t)stream;
     const bool in_place = M == 1 && N % world == 0;
+    // From here on a failure is RANK-LOCAL (this rank's shard pointer, its workspace, its kernel): the rank
+    // still takes part in the one collective — with its slice set to NaN — and returns the error after it,
+    // so its peers complete the all-gather (and see NaN columns) instead of blocking in it.
+    int local_rc = QG_OK;
     float* recv = C;
+    void* tmp = nullptr;
     if (!in_place) {
         const size_t need = qg_sharded_gemm_workspace_size(M, N, world);
-        if (!ws || ws_bytes < need || ((uintptr_t)ws & 15) != 0) return QG_ERR_UNSUPPORTED;
-        recv = static_cast<float*>(ws);
+        if (ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0) {
+            recv = static_cast<float*>(ws);
+        } else {  // a receive buffer for the collective only; the call fails
+            local_rc = QG_ERR_UNSUPPORTED;
+            if (hipMallocAsync(&tmp, need, st) != hipSuccess) return QG_ERR_HIP;  // cannot take part at all
+            recv = static_cast<float*>(tmp);
+        }
     }
     float* mine = recv + (size_t)rank * count;
-    int rc = qg_sharded_gemm_w4a8_local(A, B_shard, mine, M, N, K, wtype, world, rank, stream);
-    if (rc != QG_OK) return rc;
-    rc = nccl_status(ncclAllGather(mine, recv, count, ncclFloat32, (ncclComm_t)comm, st));
-    if (rc != QG_OK) return rc;
-    if (!in_place) {
+    if (local_rc == QG_OK && rows > 0 && !B_shard) local_rc = QG_ERR_INVALID_ARG;
+    if (local_rc == QG_OK) local_rc = qg_sharded_gemm_w4a8_local(A, B_shard, mine, M, N, K, wtype, world, rank, stream);
+    if (local_rc != QG_OK) (void)hipMemsetD32Async(mine, 0x7FC00000, count, st);  // quiet NaN
+    int rc = nccl_status(ncclAllGather(mine, recv, count, ncclFloat32, (ncclComm_t)comm, st));
+    if (rc == QG_OK && local_rc == QG_OK && !in_place) {
         const long total = (long)M * N;
         hipLaunchKernelGGL(shard_reorder_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                            (const float*)recv, C, M, N, (int)P);
-        if (hipGetLastError() != hipSuccess) return QG_ERR_HIP;
+        if (hipGetLastError() != hipSuccess) rc = QG_ERR_HIP;
     }
-    return QG_OK;
+    if (tmp) (void)hipFreeAsync(tmp, st);
+    return local_rc != QG_OK ? local_rc : rc;
 }
 
 int qg_shard_all_gather_f32(const float* send, float* recv, size_t count, qg_nccl_comm_t comm, qg_stream_t stream) {

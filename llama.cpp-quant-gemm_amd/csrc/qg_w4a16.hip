@@ -1601,7 +1601,8 @@ template <int F, int RT, int TT, int KB> hipError_t w16_sk_launch(const GemmArgs
 #define QG_W16D_MAXK 8192  // beyond, the split-K kernel is faster (K = 14336: 30.4 vs 29.4 us, ab_w16d_v2.txt)
 #endif
 // 8 < M <= 32 tokens, K % 256 == 0 (16-B aligned weight rows), 16-B aligned operands, 32-bit strides.
-// One dispatch round only (<= 256 workgroups): with more, each CU runs several workgroups in turn
+// One dispatch round only (<= one workgroup per CU: device_cus(), 256 on a whole MI355X): with more, each
+// CU runs several workgroups in turn
 // (one fits at a time) and the split-K kernel is faster (M = 32, N = 11008: 29.6 vs 23.5 us,
 // profiles/r04_tuning/ab_w16d_v1.txt).
 inline bool w16d_ok(const GemmArgs& g) {
@@ -1609,14 +1610,16 @@ inline bool w16d_ok(const GemmArgs& g) {
           ((uintptr_t)g.B & 15) == 0 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX))
         return false;
     const long rows = (g.N + 15) / 16 * ((g.M + 15) / 16);  // 16-row tiles
-    return (rows <= 256 || (long)((g.N + 31) / 32) * ((g.M + 15) / 16) <= 256) && g.K <= QG_W16D_MAXK &&
+    const long cus = device_cus();
+    return (rows <= cus || (long)((g.N + 31) / 32) * ((g.M + 15) / 16) <= cus) && g.K <= QG_W16D_MAXK &&
            (long)g.M * g.K * 4 < 0x7FFFFFF0L && (long)g.N * (g.K / QK) * wfmt<FMT_Q8_0>::BB < 0x7FFFFFF0L;  // buffer ranges
 }
 #ifndef QG_W16D_W
 // waves per workgroup (stage slots per wave: the most that fit): 16 waves with one slot each
-// (profiles/r04_tuning/ab_waves_r4v.txt, M = 32: 10.80 -> 10.15 us, M = 24 10.34 -> 9.52, M = 16
-// 8.54 -> 8.40, W8A16 10.81 -> 10.11, K = 8192 18.47 -> 17.57 against 12 waves with two slots, which beat
-// 8 waves with three: ab_w16d_waves.txt, 11.75 -> 10.78) — more waves per SIMD overlap one wave's DMA
+// (profiles/r04_tuning/ab_waves_r4v.txt, W4A16 M = 32: 10.80 -> 10.15 us, M = 24 10.34 -> 9.52, M = 16
+// 8.54 -> 8.40, K = 8192 18.47 -> 17.57 against 12 waves with two slots, which beat 8 waves with three:
+// ab_w16d_waves.txt, 11.75 -> 10.78; that record's `wtype=8` row timed the W4A16 kernel, DESIGN.md §6, so
+// the W8A16 (Q8_0) wave count is inherited from Q4_0, not separately tuned) — more waves per SIMD overlap one wave's DMA
 // wait with another's VALU; the refill of a wave's slot is issued right after its LDS reads, before the
 // stage's compute
 #define QG_W16D_W 16
@@ -1642,8 +1645,8 @@ hipError_t w16d_launch_np(const GemmArgs& g, hipStream_t st) {
                        (const uint8_t*)g.B, g.C, g.M, g.N, g.K, (int)g.ldc_m, (int)g.ldc_n);
     return hipGetLastError();
 }
-// 16-row tiles while their grid fits one dispatch round (<= 256 workgroups), else 32-row ones (w16d_ok)
-inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 15) / 16) * ((g.M + 15) / 16) > 256; }
+// 16-row tiles while their grid fits one dispatch round (<= one workgroup per CU), else 32-row ones (w16d_ok)
+inline bool w16d_rt2(const GemmArgs& g) { return (long)((g.N + 15) / 16) * ((g.M + 15) / 16) > device_cus(); }
 // Q4_0 from K = 4096 (>= 32 four-block stages, so each of 12 waves takes two or three): 4-block stages
 // with 12 waves (profiles/r04_tuning/ab_w16d_sb4*.txt: M = 32 10.12 -> 9.90 us, M = 16 8.38 -> 8.19,
 // M = 12 8.20 -> 8.06, K = 8192 17.54 -> 17.25, M = 20 / 24 +0.8 / +1.3 %; K = 1024 +8 %: 8 stages for 12

@@ -223,8 +223,19 @@ class NativeRowShardedW4A8:
     def forward(self, act_q: torch.Tensor, M: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         import ctypes
         dev = self.weight.device
+        #  everything the C library would read or write through these raw pointers is checked
+        # here first: a wrong M or a strided `out` would otherwise be an out-of-bounds device access
+        if M < 0:
+            raise RuntimeError(f"M must be >= 0, got {M}")
+        if not (act_q.is_cuda and act_q.device == dev and act_q.dtype == torch.uint8 and act_q.is_contiguous()):
+            raise RuntimeError("act_q must be a contiguous uint8 tensor on the weights' device")
+        if act_q.numel() < M * (self.K // 32) * 36:
+            raise RuntimeError(f"act_q holds {act_q.numel()} bytes, M={M} needs {M * (self.K // 32) * 36}")
         if out is None:
             out = torch.empty((M, self.n_total), dtype=torch.float32, device=dev)
+        elif not (out.is_cuda and out.device == dev and out.dtype == torch.float32 and out.is_contiguous()
+                  and tuple(out.shape) == (M, self.n_total)):
+            raise RuntimeError(f"out must be a contiguous float32 [{M}, {self.n_total}] tensor on the weights' device")
         ws = self.workspace(M)
         P = ctypes.c_void_p
         st = P(torch.cuda.current_stream(dev).cuda_stream)

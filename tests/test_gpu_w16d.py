@@ -66,7 +66,8 @@ def test_w16d_two_part_split_error(O, qg, t, m, n, k):
 
 
 def test_w16d_repeat_bit_identical(O, qg):
-    """Fixed-order sum of the 8 waves' partial tiles: repeated launches are bit-identical."""
+    """Fixed-order sum of the waves' partial tiles (12 or 16 waves, qg_w4a16.hip w16d_launch): repeated launches
+    are bit-identical."""
     m, n, k = 32, 4096, 4096
     a, b = O.fill_uniform_step4(m, n, k, seed=9)
     bq = O.quantize(b, 2)
