@@ -229,7 +229,8 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     return res
 
 
-def measure_floor(dev, wcopies: torch.Tensor, G: int, launch_bytes: int, grid: int, block: int) -> dict:
+def measure_floor(dev, wcopies: torch.Tensor, G: int, launch_bytes: int, grid: int, block: int,
+                  unit_shape=None) -> dict:
     """The single-launch floor under the headline's protocol (hipGraph of G back-to-back launches,
     HIP events on the launch stream): an empty kernel with the GEMV's grid and block, and the
     fastest pure coalesced read of the GEMV's algorithmic bytes per launch over the same rotating
@@ -263,8 +264,28 @@ def measure_floor(dev, wcopies: torch.Tensor, G: int, launch_bytes: int, grid: i
     reads = {f"x4 p{p} wg{blk}": min(graph_time_us(reader(p, blk), 10, G) for _ in range(3))
              for (p, blk) in ((1, 512), (1, 1024), (2, 512), (2, 1024), (4, 256))}
     best = min(reads, key=reads.get)
-    return {"empty_us": round(empty_us, 3), "read_us": round(reads[best], 3), "read_config": best,
-            "read_all_us": {k: round(v, 3) for k, v in reads.items()}, "grid": grid, "block": block}
+    res = {"empty_us": round(empty_us, 3), "read_us": round(reads[best], 3), "read_config": best,
+           "read_all_us": {k: round(v, 3) for k, v in reads.items()}, "grid": grid, "block": block}
+    if unit_shape is not None:
+        # the GEMV's own load shape: 36-B units per lane, 16 rows per 1024-thread
+        # workgroup, XCD tile order — without, then with, its 4-B-per-row output store
+        n_rows, k = unit_shape
+        lib.qg_calib_read_units.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        ubuf = torch.empty(n_rows, dtype=torch.float32, device=dev)
+
+        def units(store: bool):
+            def fn() -> None:
+                cs = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_calib_read_units(ctypes.c_void_p(bases[j]), n_rows, k,
+                                               ctypes.c_void_p(ubuf.data_ptr()) if store else None,
+                                               ctypes.c_void_p(sink.data_ptr()), cs) != 0:
+                        raise RuntimeError("qg_calib_read_units failed")
+            return fn
+        res["units_read_us"] = round(min(graph_time_us(units(False), 10, G) for _ in range(3)), 3)
+        res["units_read_store_us"] = round(min(graph_time_us(units(True), 10, G) for _ in range(3)), 3)
+    return res
 
 
 def algo_bytes(m: int, n: int, k: int, bb: int) -> int:
@@ -796,7 +817,8 @@ def main() -> None:
     floor = None
     if graphs is not None and not args.no_floor:
         rpb = 16  # the M = 1 GEMV's rows per 1024-thread workgroup (qg_gemv.hip)
-        floor = measure_floor(dev, wcopies, G, algo_bytes(M, local, K, bb), (local + rpb - 1) // rpb, 1024)
+        floor = measure_floor(dev, wcopies, G, algo_bytes(M, local, K, bb), (local + rpb - 1) // rpb, 1024,
+                              unit_shape=(local, K) if (M == 1 and wtype == 2 and K <= 4096 and K % 64 == 0) else None)
 
     # ---- N > 1: the step's all-gather alone (same bytes, no GEMVs beside it), so the per-GPU kernel
     #      time and the gather latency are reported separately (SURVEY.md §7, 8-GPU hard part)
@@ -878,8 +900,9 @@ def main() -> None:
                          "floor_frac": None if floor is None else round(launch_bytes / floor["read_us"] / 1e3 / HBM_PEAK_GBPS, 4),
                          "floor": None if floor is None else dict(floor, note=(
                              "single-launch floor, same protocol: empty kernel with the GEMV grid, and the fastest "
-                             "pure 16-B coalesced read of bytes_per_launch per launch over the same rotating copies "
-                             "(libqg_calib.so)"))},
+                             "pure 16-B coalesced read of bytes_per_launch per launch over the same rotating copies; "
+                             "units_read(_store)_us: the GEMV's own 36-B-unit load shape and grid without its "
+                             "arithmetic, without / with its output store (libqg_calib.so)"))},
             "batched": None if batched_us is None else {
                 "us_per_gemv": round(batched_us, 3),
                 "tflops": round(flops_per_gemv / world / batched_us / 1e6, 3),
@@ -914,6 +937,7 @@ def main() -> None:
             del mods, wcopies
             torch.cuda.empty_cache()
             sides = [("q4_0", 32, 4096, 4096, ("single", "tiled"), "configs[2]"),
+                     ("q4_0", 1, 4096, 4096, ("tiled",), "configs[1] on the tiled layout (decode GEMV)"),
                      ("q4_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q5_0", 1, 4096, 4096, ("single",), "configs[3]"), ("q5_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q4_0", 1, 32000, 4096, ("single", "batched"), "configs[4] on one GPU"),

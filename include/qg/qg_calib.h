@@ -26,6 +26,11 @@ int qg_calib_empty(int grid, int block, qg_stream_t stream);
  * read is compared against a constant and only then written to *sink (never, in practice), so the
  * loads cannot be removed and the kernel stores nothing. */
 int qg_calib_read(const void* src, size_t bytes, int loads_per_thread, int block, uint32_t* sink, qg_stream_t stream);
+/* The M = 1 Q4_0 GEMV's load shape (gemv1_kernel<2, 2, 64, 1024>) without its arithmetic: N weight rows of
+ * K/64 36-B units (K <= 4096), 16 rows per 1024-thread workgroup, lane l of row r loading unit l with 9
+ * dword loads, the GEMV's XCD-aware tile order. out != NULL: each row also stores one float to out[r]
+ * (the GEMV's output write); out == NULL: nothing stored (XOR into *sink as qg_calib_read). */
+int qg_calib_read_units(const void* B, int N, int K, float* out, uint32_t* sink, qg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -427,17 +427,14 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 // tile prefix table (a lane-parallel vector load + ballot, or 64 scalar compares): 1.72 / 2.10 us per
 // GEMV in a group of 64 vs 1.44 for the strided batch (the lookup sat in front of every workgroup's
 // weight stream).
-// Uniform groups (grp.tpi > 0: every item has tpi tiles, count % 8 == 0) run on a 1-D grid with an
-// item-per-XCD order: workgroup L is dispatched to XCD L % 8, and XCD x runs items x, x + 8, ... one
-// after the other, each item's tiles in order over its 32 CUs — so a CU sees 1/8 of the items, their
-// descriptors stay in its scalar cache (a first-touch descriptor load sits in front of every
-// workgroup's weight stream otherwise), and an item's activations and output lines stay in one XCD's L2.
-// (Mixed groups keep the 2-D grid: blockIdx.y = item, blockIdx.x its tile, XCD-aware within the item.)
-#ifndef QG_GEMVG_XCD
-// item-per-XCD order for uniform groups (A/B knob; off: profiles/r04_tuning — 64 GEMVs per grouped
-// launch 1.59 -> 1.64 us per GEMV with it)
-#define QG_GEMVG_XCD 0
-#endif
+// Shared activations (SA, round 5): when every item reads the same A (a layer's
+// Q / K / V or gate / up projections of one token batch — the usual case) the host puts that pointer in
+// the descriptor's header, which sits in the preloaded kernel-argument SGPRs: the activation staging's
+// loads then go out before the item's descriptor (an s_load from the argument segment) returns, instead
+// of waiting for it. Groups whose items all have the launch's row-tile count (grp.full) skip the
+// early-exit test, so nothing before the weight stream waits on the descriptor at all.
+// (The round-4 item-per-XCD 1-D grid for uniform groups measured slower, 1.59 -> 1.64 us per GEMV, and is
+// gone.)
 // row tiles per workgroup of the loop-free launches (gemv_body TPW): grouped (QG_GEMVG_TPW) and strided
 // batch (QG_GEMV_TPW). profiles/r04_tuning/r04d_bench_tpw*.json, 64 GEMVs (M = 1, N = K = 4096) per
 // launch: grouped 1.606 -> 1.529 us per GEMV with 2 (one descriptor load and one activation staging per
@@ -462,25 +459,18 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMVG_WDIV
 #define QG_GEMVG_WDIV 2  // grouped launch workgroup size = the single launch's / QG_GEMVG_WDIV (below)
 #endif
-template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
+template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1, bool SA = false>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     constexpr int RPB = (WGS / 64) * (64 / LPR) * TPW;  // rows per workgroup
-    int item, tile;
-    if (grp.tpi > 0) {
-        const int L = blockIdx.x, j = L >> 3;
-        item = 8 * (j / grp.tpi) + (L & 7);
-        tile = j - (j / grp.tpi) * grp.tpi;
-    } else {
-        item = blockIdx.y;
-        // the single launch's XCD-aware tile order (gemv_body) within the item: with grid.x a multiple
-        // of 8 the workgroup's XCD is blockIdx.x % 8, so each XCD takes a contiguous range of its tiles
-        tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    }
+    const int item = blockIdx.y;
+    // the single launch's XCD-aware tile order (gemv_body) within the item: with grid.x a multiple of 8 the
+    // workgroup's XCD is blockIdx.x % 8, so each XCD takes a contiguous range of its tiles
+    const int tile = gridDim.x <= 512 ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const GemvItemDesc d = grp.it[item];
-    if (tile * RPB >= d.N) return;  // past this item's rows (uniform)
+    if (!grp.full && tile * RPB >= d.N) return;  // past this item's rows (uniform)
     gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, TPW>(
-        reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K, d.C, 0,
-        d.ldc, 1, nullptr, tile);
+        reinterpret_cast<const uint32_t*>(SA ? grp.A : d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K,
+        d.C, 0, d.ldc, 1, nullptr, tile);
 }
 
 // Host side -------------------------------------------------------------------------------------
@@ -533,17 +523,18 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                     tiles = std::max(tiles, t);
                     tmin = std::min(tmin, t);
                 }
-                auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP>
-                              : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false>;
+                const bool sa = grp.A != nullptr;
+                auto kg = one ? (sa ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP, true>
+                                    : gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP, false>)
+                              : (sa ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false, 1, true>
+                                    : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false, 1, false>);
                 if (lds > 64 * 1024) {
                     hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                     if (e != hipSuccess) return e;
                 }
                 if (tiles == 0 || grp.count == 0) return hipSuccess;
-                const bool uniform = QG_GEMVG_XCD && tiles == tmin && grp.count % 8 == 0 && (long)tiles * grp.count <= INT32_MAX;
-                grp.tpi = uniform ? tiles : 0;
-                const dim3 grid = uniform ? dim3(tiles * grp.count) : dim3(tiles, grp.count);
-                hipLaunchKernelGGL(kg, grid, dim3(GW), lds, st, grp);
+                grp.full = tiles == tmin ? 1 : 0;
+                hipLaunchKernelGGL(kg, dim3(tiles, grp.count), dim3(GW), lds, st, grp);
                 return hipGetLastError();
             };
             // workgroups of WGS / QG_GEMVG_WDIV threads while the largest item's rows fit one round of

@@ -48,9 +48,11 @@ struct GemvItemDesc {  // 32 B: one s_load_dwordx8 in the kernel
     int N, ldc;
 };
 struct GemvGroup {
-    // tpi > 0: every item has tpi row tiles and count % 8 == 0, the grid is 1-D (count * tpi) and
-    // workgroup L runs item 8 (L / 8 / tpi) + L % 8, tile (L / 8) % tpi (qg_gemv_kernel.hpp, gemvg_kernel)
-    int count, M, K, tpi;
+    // A: non-null when every item reads the same activations (then it is the items' A_q8_1, read from the
+    // preloaded header instead of each item's record); full: every item has the launch's row-tile count
+    // (no workgroup exits early) — qg_gemv_kernel.hpp, gemvg_kernel
+    const void* A;
+    int count, M, K, full;
     GemvItemDesc it[GEMV_GROUP_MAX];
 };
 
@@ -85,6 +87,11 @@ hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
 // MFMA-assisted (v_mfma_f32_16x16x16_f16) scale epilogue.
 bool mfma_eligible(const GemmArgs& g);
 hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
+
+// The decode GEMV (M <= 4) on the tiled layout (qg_gemvt.hip): per-block terms bit-identical to the
+// reference's, fixed summation order.
+bool gemvt_eligible(const GemmArgs& g);
+hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st);
 
 // Any shape / alignment with K % 32 == 0 (byte-granular loads); also the debug sumi fallback.
 hipError_t launch_generic(const GemmArgs& g, hipStream_t st);

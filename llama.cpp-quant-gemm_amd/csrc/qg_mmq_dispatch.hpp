@@ -45,8 +45,18 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 // (M = 16 6.58 -> 7.15 with 16 waves: its 34-byte blocks double the per-stage ingest). The 8-wave
 // 32 x 32 tiles (M > 32) keep 8 x 2: 12 or 16 waves exceed the VGPR budget of their accumulators
 // (ab_waves_r4x.txt: M = 64 9.8 -> 24-55 us).
-template <int F, int BN, int TT> constexpr int alt_w = BN == 32 && TT == 1 ? 12 : BN == 16 ? (F != FMT_Q8_0 ? 16 : 8) : 8;
-template <int F, int BN, int TT> constexpr int alt_nb = BN == 32 && TT == 1 ? 1 : BN == 16 ? (F != FMT_Q8_0 ? 1 : 2) : 2;
+// The tiled layout's 32 x 16 tile (LAY_TILED): QG_MMQ_TILED_W waves x QG_MMQ_TILED_NB slots (a tuning
+// choice only: every value computes the same bits — tests/test_gpu_tiled.py).
+#ifndef QG_MMQ_TILED_W
+#define QG_MMQ_TILED_W 12
+#endif
+#ifndef QG_MMQ_TILED_NB
+#define QG_MMQ_TILED_NB 1
+#endif
+template <int F, int BN, int TT, int LAY>
+constexpr int alt_w = BN == 32 && TT == 1 ? (LAY == LAY_TILED ? QG_MMQ_TILED_W : 12) : BN == 16 ? (F != FMT_Q8_0 ? 16 : 8) : 8;
+template <int F, int BN, int TT, int LAY>
+constexpr int alt_nb = BN == 32 && TT == 1 ? (LAY == LAY_TILED ? QG_MMQ_TILED_NB : 1) : BN == 16 ? (F != FMT_Q8_0 ? 1 : 2) : 2;
 
 // grid of one dispatch round: at most one workgroup per CU (device_cus(): 256 on a whole MI355X)
 inline bool one_round(const GemmArgs& g, int BN, int NTOK) {
@@ -55,8 +65,8 @@ inline bool one_round(const GemmArgs& g, int BN, int NTOK) {
 
 template <int F, int BN, int TT, int W, bool P16, int LAY, bool AW> hipError_t run_p(const GemmArgs& g, hipStream_t st) {
     constexpr bool S = short_sig<BN, TT, W> && LAY == LAY_ROWS && !AW;
-    if constexpr (W == 8 && (alt_w<F, BN, TT> != 8 || alt_nb<F, BN, TT> != 2)) {
-        constexpr int W2 = alt_w<F, BN, TT>, NB2 = alt_nb<F, BN, TT>;
+    if constexpr (W == 8 && (alt_w<F, BN, TT, LAY> != 8 || alt_nb<F, BN, TT, LAY> != 2)) {
+        constexpr int W2 = alt_w<F, BN, TT, LAY>, NB2 = alt_nb<F, BN, TT, LAY>;
         using G2 = mmq_geom<F, BN, TT, W2, P16, NB2, LAY, AW>;
         constexpr bool fits = (size_t)W2 * NB2 * G2::BUF <= 160 * 1024 && (size_t)W2 * G2::NACC * 256 <= 160 * 1024;
         if constexpr (fits) {

@@ -26,7 +26,23 @@ def main() -> None:
     ap.add_argument("--shapes", default="32x4096x4096:2,16x4096x4096:2,8x4096x4096:2,64x4096x4096:2,128x4096x4096:2")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--G", type=int, default=64)
+    ap.add_argument("--libs", nargs="*", default=[], help="variant builds of libqg_hip.so: their tiled entry is timed too")
+    ap.add_argument("--rows-libs", nargs="*", default=[], help="other builds whose reference-row entry is timed too")
     a = ap.parse_args()
+    import ctypes
+    P = ctypes.c_void_p
+    extra = {}
+    for path in a.libs + a.rows_libs:
+        lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
+        tag = os.path.basename(path).replace("libqg_", "").replace(".so", "")
+        if path in a.libs:
+            f = lib.qg_gemm_w4a8_tiled
+            f.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+            extra["tiled@" + tag] = ("tiled", f)
+        else:
+            f = lib.qg_gemm_w4a8_ex
+            f.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+            extra["rows@" + tag] = ("rows", f)
     dev = torch.device("cuda", 0)
     for spec in a.shapes.split(","):
         dims, wt = spec.split(":")
@@ -51,14 +67,27 @@ def main() -> None:
         ref = qg.gemm_w4a8(aq, wq, M, N, K, wt)
 
         def step_of(name):
+            if name in extra:
+                kind, f = extra[name]
+                cp = copies[kind]
+
+                def run():
+                    cs = P(torch.cuda.current_stream().cuda_stream)
+                    for j in range(a.G):
+                        args = (P(aq.data_ptr()), P(cp[j].data_ptr()), P(out[j].data_ptr()), M, N, K, wt)
+                        rc = f(*args, cs) if kind == "tiled" else f(*args, 0, cs)
+                        if rc != 0:
+                            raise RuntimeError(f"{name}: status {rc}")
+                return run
             cp = copies[name]
             if name == "rows":
                 return lambda: [qg.gemm_w4a8(aq, cp[j], M, N, K, wt, out=out[j]) for j in range(a.G)]
             return lambda: [qg.gemm_w4a8_tiled(aq, cp[j], M, N, K, wt, out=out[j]) for j in range(a.G)]
 
-        times = {n: [] for n in forms}
+        names = list(forms) + [n for n, (kind, _) in extra.items() if kind in copies]
+        times = {n: [] for n in names}
         for _ in range(a.rounds):
-            for n in forms:
+            for n in names:
                 times[n].append(graph_time_us(step_of(n), 10, a.G))
         same = bool(torch.equal(qg.gemm_w4a8_tiled(aq, wt_t, M, N, K, wt), ref))
         print(f"M={M} N={N} K={K} wtype={wt}: " + "  ".join(
