@@ -200,7 +200,13 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1>
+// CO (coalesced weight read, round 5 A/B; one row per wave, loop-free, 16-B aligned rows of RB % 16 == 0
+// bytes): the wave reads its row as lane-contiguous 16-B pieces (piece p = lane + 64 j: 1 KiB per load
+// instruction instead of 36-B units at a 36-B stride), parks them in a wave-private LDS slot behind the
+// activation records and each lane reads its unit back (wave-local: LDS operations of one wave complete in
+// order) — the floor read's access shape with the unit decode unchanged.
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1,
+          bool CO = false>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
                                           int32_t* __restrict__ sumi_out, int tile_in = -1) {
@@ -258,7 +264,19 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     auto rec_of = [&](int blk) { return (blk / BPL) * G::REC_DW + (blk % BPL) * 12; };
     uint32_t cur[G::UDW];
     uint32_t more[TPW > 1 ? TPW - 1 : 1][G::UDW];  // tiles 1.. of the workgroup (TPW > 1)
+    static_assert(!CO || (LPR == 64 && ONEU && TPW == 1 && !NT), "coalesced read: one row per wave, loop-free");
+    const int npc = U * G::UB / 16;  // CO: 16-B pieces per row
+    uint4 wp[CO ? (64 * G::UB + 1023) / 1024 : 1];
     auto load_first = [&]() {
+        if constexpr (CO) {
+            const uint4* rp = reinterpret_cast<const uint4*>(wrows[0]);
+#pragma unroll
+            for (int j = 0; j < (64 * G::UB + 1023) / 1024; ++j) {
+                const int p = lane + 64 * j;
+                wp[j] = p < npc ? rp[p] : make_uint4(0u, 0u, 0u, 0u);
+            }
+            return;
+        }
         load_unit(cur, lir);
 #pragma unroll
         for (int t = 1; t < TPW; ++t) load_unit(more[t - 1], lir, t);
@@ -348,7 +366,19 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
         // tiles 1.. after tile 0 (below): the records read once, each tile its own sum and store
         static_assert(!SUMI || TPW == 1, "parity hook: one tile per workgroup");
     }
-    if constexpr (ONEU) {
+    if constexpr (ONEU && CO) {
+        read_pre(lir);
+        uint32_t* slot = lds + (M * U * G::REC_DW + 3) / 4 * 4 + (tid >> 6) * (64 * G::UB / 4);
+#pragma unroll
+        for (int j = 0; j < (64 * G::UB + 1023) / 1024; ++j) {
+            const int p = lane + 64 * j;
+            if (p < npc) *reinterpret_cast<uint4*>(slot + 4 * p) = wp[j];
+        }
+        asm volatile("" ::: "memory");  // the unit reads stay behind the piece writes (in order in the LDS)
+#pragma unroll
+        for (int v = 0; v < G::UDW; ++v) cur[v] = slot[lir * G::UDW + v];
+        if (lir < U) dot_unit(cur, lir, row, row_ok);
+    } else if constexpr (ONEU) {
         if (lir < U) do_unit(lir);
     } else {
         for (int j = 0; j < iters; ++j) {
@@ -410,10 +440,10 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
 // entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
-template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
+template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false, bool CO = false>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
-    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, 1, CO>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 
@@ -557,13 +587,20 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
         }
     }
     if (m1) {
-        auto k1 = one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
-        if (lds > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+#ifndef QG_GEMV1_CO
+#define QG_GEMV1_CO 0  // coalesced weight read of the M = 1 entry (gemv_body CO; A/B)
+#endif
+        constexpr bool CO_OK = QG_GEMV1_CO && LPR == 64;
+        const bool co = CO_OK && one && ((uintptr_t)g.B & 15) == 0 && (g.K / QK / BPL) * gemv_geom<F, BPL>::UB % 16 == 0;
+        auto k1 = co ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true, CO_OK>
+                : one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
+        const size_t lds1 = co ? (gemv_lds_bytes<F, BPL>(g.M, g.K) + 15) / 16 * 16 + (WGS / 64) * 64 * gemv_geom<F, BPL>::UB : lds;
+        if (lds1 > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
             if (e != hipSuccess) return e;
         }
         void* out = SUMI ? (void*)g.sumi : (void*)g.C;
-        hipLaunchKernelGGL(k1, dim3(grid), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.N, g.K, out);
+        hipLaunchKernelGGL(k1, dim3(grid), dim3(WGS), lds1, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.N, g.K, out);
         return hipGetLastError();
     }
     // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)

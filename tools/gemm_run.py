@@ -25,6 +25,7 @@ def main() -> None:
     ap.add_argument("--wtype", type=int, default=2)
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--w16", action="store_true", help="FP32 activations through qg_gemm_w4a16_ws (Q4_0) / w8a16 (Q8_0)")
+    ap.add_argument("--tiled", action="store_true", help="the tiled weight layout (qg_tile_weights + qg_gemm_w4a8_tiled)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -32,6 +33,8 @@ def main() -> None:
     x = torch.rand((a.m, a.k), generator=g, device=dev) * 2 - 1
     w = torch.rand((a.n, a.k), generator=g, device=dev) * 2 - 1
     xq, wq = qg.quantize_q8_1(x), qg.quantize(w, a.wtype)
+    if a.tiled:
+        wq = qg.tile_weights(wq, a.n, a.k, a.wtype)
     R = max(2, math.ceil(600e6 / wq.numel()))
     copies = torch.empty((R,) + tuple(wq.shape), dtype=torch.uint8, device=dev)
     copies.copy_(wq.unsqueeze(0).expand_as(copies))
@@ -46,6 +49,9 @@ def main() -> None:
         if a.w16:
             rc = fn(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()), ctypes.c_void_p(out.data_ptr()),
                     a.m, a.n, a.k, ctypes.c_void_p(ws.data_ptr()), wsb, st)
+        elif a.tiled:
+            rc = lib.qg_gemm_w4a8_tiled(ctypes.c_void_p(xq.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
+                                        ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)
         else:
             rc = lib.qg_gemm_w4a8(ctypes.c_void_p(xq.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
                                   ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)

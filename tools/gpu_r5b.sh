@@ -12,3 +12,4 @@ cat gpurun_out/r5b_ab_grouped.txt
 timeout -k 10 200 python -u tools/ab_quant.py --libs $V/libqg_r04.so $L > gpurun_out/r5b_ab_quant.txt 2>&1 || exit 1
 cat gpurun_out/r5b_ab_quant.txt
 timeout -k 10 300 python -u bench.py > gpurun_out/r5b_bench.json 2> gpurun_out/r5b_bench.err; echo bench rc=$?
+timeout -k 10 200 python -u tools/ab_lib.py --libs $V/libqg_r04.so $L $V/libqg_co.so --shapes 1x4096x4096:2,1x4000x4096:2 --rounds 9 > gpurun_out/r5b_ab_co.txt 2>&1; cat gpurun_out/r5b_ab_co.txt

@@ -27,7 +27,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("d")
     ap.add_argument("--pmc-json")
-    ap.add_argument("--key", default="q4_0_m1_n4096_k4096")
+    ap.add_argument("--key", default="")
     args = ap.parse_args()
     out = []
     for f in sorted(glob.glob(os.path.join(args.d, "**", "*kernel_trace.csv"), recursive=True)):
@@ -55,7 +55,17 @@ def main() -> None:
         out.append(f"### counters: {os.path.relpath(f, args.d)}\n")
         out.append("| kernel | grid x,y | counter | dispatches | mean | derived |")
         out.append("|---|---|---|---|---|---|")
+        main_k, main_n = None, -1
         for (n, gx, gy), cs in groups.items():
+            nd = max(len(v) for v in cs.values())
+            if "quantize" not in n and nd > main_n:
+                main_k, main_n = f"{n}|{gx},{gy}", nd
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs:
+                # busy cycles are summed over the 1,024 SIMDs, GRBM_GUI_ACTIVE counts once per XCD (8)
+                frac = (st.mean(cs["SQ_VALU_MFMA_BUSY_CYCLES"]) / 1024) / (st.mean(cs["GRBM_GUI_ACTIVE"]) / 8)
+                pmc.setdefault(f"{n}|{gx},{gy}", {})["mfma_busy_frac"] = frac
+                out.append(f"| `{n}` | {gx},{gy} | matrix pipe busy | {len(cs['GRBM_GUI_ACTIVE'])} | {frac:.4f} | "
+                           f"(SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs) |")
             for c, v in cs.items():
                 derived = ""
                 if c == "FETCH_SIZE":
@@ -66,6 +76,8 @@ def main() -> None:
                     pmc.setdefault(f"{n}|{gx},{gy}", {})["hbm_write_bytes_per_launch"] = st.mean(v) * 1024
                 out.append(f"| `{n}` | {gx},{gy} | {c} | {len(v)} | {st.mean(v):.1f} | {derived} |")
         out.append("")
+        if args.key and main_k in pmc:  # the config's main kernel (most dispatches) under the config key
+            pmc[args.key] = dict(pmc[main_k], kernel=main_k)
     print("\n".join(out))
     if args.pmc_json and pmc:
         json.dump(pmc, open(args.pmc_json, "w"), indent=1)
