@@ -130,8 +130,9 @@ int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, i
  * restated in oracle/oracle.py (tile_weights); one streaming kernel.
  * qg_gemm_w4a8_tiled then computes the same product as qg_gemm_w4a8(A, B, ...) (activation-major,
  * A: block_q8_1 [M][K/32], 16-B aligned; within the reassociation bound of the MFMA kernel, DESIGN.md
- * §5) from B_tiled in ONE launch for every M — the prefill's weight stages are one linear stream
- * instead of 32 row segments. K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
+ * §5; at M = 1 the tiled decode GEMV, whose per-block terms are the reference's bit for bit) from B_tiled
+ * in ONE launch for every M — the prefill's weight stages are one linear stream instead of 32 row
+ * segments (decode-heavy callers: the reference rows' GEMV stays faster at M = 1). K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
  * activation rows). _ldc: output row stride (>= N floats). qg_debug_sumi_tiled / qg_debug_config_tiled
  * are the parity hook and the configuration query of the same instantiation (as qg_debug_sumi /
  * qg_debug_config below). Replaces the tiled-GEMM role of include/gemm_cuda_tiled.cuh:293-300 and the

@@ -225,7 +225,7 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     return QG_OK;
 }
 
-// The tiled weight layout (qg_tile_weights): the tiled decode GEMV for M <= 4 (qg_gemvt.hip), the MFMA
+// The tiled weight layout (qg_tile_weights): the tiled decode GEMV for M = 1 (qg_gemvt.hip), the MFMA
 // kernel beyond (LAY_TILED; odd K/32 through its activation windows).
 int run_tiled(GemmArgs& g, hipStream_t st) {
     if (g.M < 0 || g.N < 0) return QG_ERR_INVALID_ARG;
@@ -234,7 +234,7 @@ int run_tiled(GemmArgs& g, hipStream_t st) {
     if (g.M == 0 || g.N == 0) return QG_OK;
     if (!g.A || !g.B || (!g.C && !g.sumi)) return QG_ERR_INVALID_ARG;
     if (((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 15) != 0) return QG_ERR_ALIGN;
-    if (gemvt_eligible(g)) return hip_status(launch_gemvt(g, st));  // M <= 4: the tiled decode GEMV
+    if (gemvt_eligible(g)) return hip_status(launch_gemvt(g, st));  // M = 1: the tiled decode GEMV
     if (!mfma_eligible(g)) return QG_ERR_UNSUPPORTED;
     return hip_status(launch_mfma(g, st));
 }
@@ -607,9 +607,6 @@ int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int
             maxn = std::max(maxn, it.N);
         }
         if (grp.count == 0) break;
-        grp.A = grp.it[0].A;  // shared activations: staged before the item's descriptor arrives
-        for (int i = 1; i < grp.count; ++i)
-            if (grp.it[i].A != grp.A) grp.A = nullptr;
         GemmArgs g;
         g.A = grp.it[0].A; g.B = grp.it[0].B; g.C = grp.it[0].C; g.M = M; g.N = maxn; g.K = K; g.wtype = wtype;
         g.ldc_m = grp.it[0].ldc; g.ldc_n = 1;

@@ -40,6 +40,18 @@ __global__ __launch_bounds__(1024) void calib_units_kernel(const uint8_t* __rest
 #pragma unroll
     for (int v = 0; v < 9; ++v) x ^= p[v];
     if constexpr (STORE) {
+        // every lane's loads feed the stored value (a wave-wide XOR over DPP row ops, as the GEMV's
+        // group_sum_last): with only lane 63's value used, the compiler sank the loads under the store's
+        // lane predicate and the launch read 1/64 of the bytes
+        auto dx = [](uint32_t v, auto ctrl, auto rm) {
+            return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, decltype(ctrl)::value, decltype(rm)::value, 0xF, false);
+        };
+        x ^= dx(x, qg::ic<0xB1>{}, qg::ic<0xF>{});
+        x ^= dx(x, qg::ic<0x4E>{}, qg::ic<0xF>{});
+        x ^= dx(x, qg::ic<0x114>{}, qg::ic<0xF>{});
+        x ^= dx(x, qg::ic<0x118>{}, qg::ic<0xF>{});
+        x ^= dx(x, qg::ic<0x142>{}, qg::ic<0xA>{});
+        x ^= dx(x, qg::ic<0x143>{}, qg::ic<0xC>{});
         if (row < N && lane == 63) out[row] = __uint_as_float(x & 0x3FFFFFFFu);
     } else {
         if (x == 0x9E3779B9u && threadIdx.x == 0x3FF) sink[0] = x;

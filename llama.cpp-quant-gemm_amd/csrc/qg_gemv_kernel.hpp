@@ -200,13 +200,7 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
-// CO (coalesced weight read, round 5 A/B; one row per wave, loop-free, 16-B aligned rows of RB % 16 == 0
-// bytes): the wave reads its row as lane-contiguous 16-B pieces (piece p = lane + 64 j: 1 KiB per load
-// instruction instead of 36-B units at a 36-B stride), parks them in a wave-private LDS slot behind the
-// activation records and each lane reads its unit back (wave-local: LDS operations of one wave complete in
-// order) — the floor read's access shape with the unit decode unchanged.
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1,
-          bool CO = false>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
                                           int32_t* __restrict__ sumi_out, int tile_in = -1) {
@@ -264,19 +258,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     auto rec_of = [&](int blk) { return (blk / BPL) * G::REC_DW + (blk % BPL) * 12; };
     uint32_t cur[G::UDW];
     uint32_t more[TPW > 1 ? TPW - 1 : 1][G::UDW];  // tiles 1.. of the workgroup (TPW > 1)
-    static_assert(!CO || (LPR == 64 && ONEU && TPW == 1 && !NT), "coalesced read: one row per wave, loop-free");
-    const int npc = U * G::UB / 16;  // CO: 16-B pieces per row
-    uint4 wp[CO ? (64 * G::UB + 1023) / 1024 : 1];
     auto load_first = [&]() {
-        if constexpr (CO) {
-            const uint4* rp = reinterpret_cast<const uint4*>(wrows[0]);
-#pragma unroll
-            for (int j = 0; j < (64 * G::UB + 1023) / 1024; ++j) {
-                const int p = lane + 64 * j;
-                wp[j] = p < npc ? rp[p] : make_uint4(0u, 0u, 0u, 0u);
-            }
-            return;
-        }
         load_unit(cur, lir);
 #pragma unroll
         for (int t = 1; t < TPW; ++t) load_unit(more[t - 1], lir, t);
@@ -366,19 +348,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
         // tiles 1.. after tile 0 (below): the records read once, each tile its own sum and store
         static_assert(!SUMI || TPW == 1, "parity hook: one tile per workgroup");
     }
-    if constexpr (ONEU && CO) {
-        read_pre(lir);
-        uint32_t* slot = lds + (M * U * G::REC_DW + 3) / 4 * 4 + (tid >> 6) * (64 * G::UB / 4);
-#pragma unroll
-        for (int j = 0; j < (64 * G::UB + 1023) / 1024; ++j) {
-            const int p = lane + 64 * j;
-            if (p < npc) *reinterpret_cast<uint4*>(slot + 4 * p) = wp[j];
-        }
-        asm volatile("" ::: "memory");  // the unit reads stay behind the piece writes (in order in the LDS)
-#pragma unroll
-        for (int v = 0; v < G::UDW; ++v) cur[v] = slot[lir * G::UDW + v];
-        if (lir < U) dot_unit(cur, lir, row, row_ok);
-    } else if constexpr (ONEU) {
+    if constexpr (ONEU) {
         if (lir < U) do_unit(lir);
     } else {
         for (int j = 0; j < iters; ++j) {
@@ -440,10 +410,10 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
 // entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
-template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false, bool CO = false>
+template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
-    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU, 1, CO>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
+    gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
                                                                      1, SUMI ? (int32_t*)out : nullptr);
 }
 
@@ -457,14 +427,10 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 // tile prefix table (a lane-parallel vector load + ballot, or 64 scalar compares): 1.72 / 2.10 us per
 // GEMV in a group of 64 vs 1.44 for the strided batch (the lookup sat in front of every workgroup's
 // weight stream).
-// Shared activations (SA, round 5): when every item reads the same A (a layer's
-// Q / K / V or gate / up projections of one token batch — the usual case) the host puts that pointer in
-// the descriptor's header, which sits in the preloaded kernel-argument SGPRs: the activation staging's
-// loads then go out before the item's descriptor (an s_load from the argument segment) returns, instead
-// of waiting for it. Groups whose items all have the launch's row-tile count (grp.full) skip the
-// early-exit test, so nothing before the weight stream waits on the descriptor at all.
-// (The round-4 item-per-XCD 1-D grid for uniform groups measured slower, 1.59 -> 1.64 us per GEMV, and is
-// gone.)
+// Groups whose items all have the launch's row-tile count (grp.full) skip the early-exit test. (The
+// round-4 item-per-XCD 1-D grid for uniform groups measured slower, 1.59 -> 1.64 us per GEMV; round 5:
+// staging the activations of groups with one shared A from the preloaded header, before the item's
+// descriptor returns, measured no gain — profiles/r05_tuning/r5b_ab_grouped.txt, 1.510 -> 1.516 us.)
 // row tiles per workgroup of the loop-free launches (gemv_body TPW): grouped (QG_GEMVG_TPW) and strided
 // batch (QG_GEMV_TPW). profiles/r04_tuning/r04d_bench_tpw*.json, 64 GEMVs (M = 1, N = K = 4096) per
 // launch: grouped 1.606 -> 1.529 us per GEMV with 2 (one descriptor load and one activation staging per
@@ -489,7 +455,7 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMVG_WDIV
 #define QG_GEMVG_WDIV 2  // grouped launch workgroup size = the single launch's / QG_GEMVG_WDIV (below)
 #endif
-template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1, bool SA = false>
+template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     constexpr int RPB = (WGS / 64) * (64 / LPR) * TPW;  // rows per workgroup
     const int item = blockIdx.y;
@@ -499,7 +465,7 @@ __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     const GemvItemDesc d = grp.it[item];
     if (!grp.full && tile * RPB >= d.N) return;  // past this item's rows (uniform)
     gemv_body<F, MT, BPL, LPR, WGS, false, AIN_Q8_1, false, PRE, ONEU, TPW>(
-        reinterpret_cast<const uint32_t*>(SA ? grp.A : d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K,
+        reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K,
         d.C, 0, d.ldc, 1, nullptr, tile);
 }
 
@@ -553,11 +519,8 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
                     tiles = std::max(tiles, t);
                     tmin = std::min(tmin, t);
                 }
-                const bool sa = grp.A != nullptr;
-                auto kg = one ? (sa ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP, true>
-                                    : gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP, false>)
-                              : (sa ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false, 1, true>
-                                    : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false, 1, false>);
+                auto kg = one ? gemvg_kernel<F, MT, BPL, LPR, GW, PRE, true, TP>
+                              : gemvg_kernel<F, MT, BPL, LPR, GW, PRE && (MT <= 2), false>;
                 if (lds > 64 * 1024) {
                     hipError_t e = hipFuncSetAttribute((const void*)kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                     if (e != hipSuccess) return e;
@@ -587,20 +550,13 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
         }
     }
     if (m1) {
-#ifndef QG_GEMV1_CO
-#define QG_GEMV1_CO 0  // coalesced weight read of the M = 1 entry (gemv_body CO; A/B)
-#endif
-        constexpr bool CO_OK = QG_GEMV1_CO && LPR == 64;
-        const bool co = CO_OK && one && ((uintptr_t)g.B & 15) == 0 && (g.K / QK / BPL) * gemv_geom<F, BPL>::UB % 16 == 0;
-        auto k1 = co ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true, CO_OK>
-                : one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
-        const size_t lds1 = co ? (gemv_lds_bytes<F, BPL>(g.M, g.K) + 15) / 16 * 16 + (WGS / 64) * 64 * gemv_geom<F, BPL>::UB : lds;
-        if (lds1 > 64 * 1024) {
-            hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+        auto k1 = one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
         void* out = SUMI ? (void*)g.sumi : (void*)g.C;
-        hipLaunchKernelGGL(k1, dim3(grid), dim3(WGS), lds1, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.N, g.K, out);
+        hipLaunchKernelGGL(k1, dim3(grid), dim3(WGS), lds, st, (const uint32_t*)g.A, (const uint8_t*)g.B, g.N, g.K, out);
         return hipGetLastError();
     }
     // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)

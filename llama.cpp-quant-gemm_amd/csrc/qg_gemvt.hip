@@ -1,4 +1,4 @@
-// qg_gemvt.hip — the decode GEMV (M <= 4 tokens) on the tiled weight layout (LAY_TILED,
+// qg_gemvt.hip — the decode GEMV (M = 1 token) on the tiled weight layout (LAY_TILED,
 // qg_tile_weights; tiled_fmt in qg_mmq_kernel.hpp), so weights kept only in that layout serve the decode
 // as well as the prefill (qg_gemm_w4a8_tiled). C[M,N] = A_q8_1[M,K] . B[N,K]^T (include/gemm_reference.h:
 // 175-222), each block's fp32 term in the reference's operation order (qg_common.hpp block_term_f), i.e.
@@ -70,9 +70,14 @@ __global__ __launch_bounds__(GT_W * 64) void gemvt_kernel(const uint8_t* __restr
         for (int i = 0; i < 9; ++i) ab[i] = A32[(long)g * 9 + i];
     };
     if (tid < totb) load_ablk(tid);
+    // every stage of this wave (up to NS) in flight before the staging barrier; beyond NS (K > 8192) one
+    // stage ahead
     const int nst = wave < H ? (H - 1 - wave) / GT_W + 1 : 0;
-    wst cur, nxt;
-    if (nst > 0) load(wave, cur);
+    constexpr int NS = 4;
+    wst pre[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if (k < nst) load(wave + k * GT_W, pre[k]);
     for (int g = tid; g < totb; g += GT_W * 64) {
         if (g != tid) load_ablk(g);
 #pragma unroll
@@ -84,9 +89,7 @@ __global__ __launch_bounds__(GT_W * 64) void gemvt_kernel(const uint8_t* __restr
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
     const int n = n0 + r;
-    for (int k = 0; k < nst; ++k) {
-        const int h = wave + k * GT_W;
-        if (k + 1 < nst) load(h + GT_W, nxt);
+    auto stage = [&](const wst& cur, int h) {
         const uint32_t qv[4] = {cur.qs.x, cur.qs.y, cur.qs.z, cur.qs.w};
         const uint32_t q8[4] = {cur.qs8.x, cur.qs8.y, cur.qs8.z, cur.qs8.w};
         const uint32_t qhv[4] = {cur.qh.x, cur.qh.y, cur.qh.z, cur.qh.w};
@@ -139,7 +142,15 @@ __global__ __launch_bounds__(GT_W * 64) void gemvt_kernel(const uint8_t* __restr
                 }
             }
         }
-        if (k + 1 < nst) cur = nxt;
+    };
+    static_for<NS>([&](auto KI) {
+        constexpr int k = decltype(KI)::value;
+        if (k < nst) stage(pre[k], wave + k * GT_W);
+    });
+    for (int k = NS; k < nst; ++k) {
+        wst c;
+        load(wave + k * GT_W, c);
+        stage(c, wave + k * GT_W);
     }
     if constexpr (!SUMI) {
         // the row's 4 k-slot lanes, then the waves in fixed order
@@ -192,9 +203,12 @@ template <int F> hipError_t gemvt_f(const GemmArgs& g, hipStream_t st) {
 
 }  // namespace
 
-// M <= 4, the activation rows within the LDS, 32-bit strides (A 4-B aligned, B_tiled 16-B aligned)
+// M = 1 only: against the tiled MFMA kernel (16-row tiles) it measured 4.19-4.26 vs 4.54 us at M = 1 but
+// 4.88 vs 4.5 at M = 2 and 5.9-6.4 vs 4.5 at M = 4 (profiles/r05_tuning/r5b_ab_tiled.txt, r5c_ab_tiled.txt: the
+// per-token LDS reads and quad reductions grow with M), so M = 2..4 run the MFMA kernel. The activation
+// row within the LDS, 32-bit strides (A 4-B aligned, B_tiled 16-B aligned).
 bool gemvt_eligible(const GemmArgs& g) {
-    return g.lay == LAY_TILED && g.M >= 1 && g.M <= 4 && g.N >= 1 && g.K % QK == 0 && ((uintptr_t)g.B & 15) == 0 &&
+    return g.lay == LAY_TILED && g.M == 1 && g.N >= 1 && g.K % QK == 0 && ((uintptr_t)g.B & 15) == 0 &&
            ((uintptr_t)g.A & 3) == 0 && (size_t)g.M * (g.K / QK) * 36 <= 144 * 1024 && g.ldc_m <= INT32_MAX &&
            g.ldc_n <= INT32_MAX && (long)g.M * g.N * (g.K / QK) < (1L << 62);
 }

@@ -48,10 +48,7 @@ struct GemvItemDesc {  // 32 B: one s_load_dwordx8 in the kernel
     int N, ldc;
 };
 struct GemvGroup {
-    // A: non-null when every item reads the same activations (then it is the items' A_q8_1, read from the
-    // preloaded header instead of each item's record); full: every item has the launch's row-tile count
-    // (no workgroup exits early) — qg_gemv_kernel.hpp, gemvg_kernel
-    const void* A;
+    // full: every item has the launch's row-tile count (no workgroup exits early) — gemvg_kernel
     int count, M, K, full;
     GemvItemDesc it[GEMV_GROUP_MAX];
 };
