@@ -90,9 +90,20 @@ def main() -> None:
             for n in names:
                 times[n].append(graph_time_us(step_of(n), 10, a.G))
         same = bool(torch.equal(qg.gemm_w4a8_tiled(aq, wt_t, M, N, K, wt), ref))
+        bits = {}
+        for name, (kind, f) in extra.items():  # each variant's output against the in-tree reference rows
+            if kind not in copies:
+                continue
+            o = torch.zeros((M, N), dtype=torch.float32, device=dev)
+            w = wt_t if kind == "tiled" else wq
+            cs = P(torch.cuda.current_stream().cuda_stream)
+            args = (P(aq.data_ptr()), P(w.data_ptr()), P(o.data_ptr()), M, N, K, wt)
+            rc = f(*args, cs) if kind == "tiled" else f(*args, 0, cs)
+            torch.cuda.synchronize()
+            bits[name] = "rc%d" % rc if rc else ("==" if torch.equal(o, ref) else "max|d| %.3g" % float((o - ref).abs().max()))
         print(f"M={M} N={N} K={K} wtype={wt}: " + "  ".join(
             f"{n} {statistics.median(v):.3f} us (min {min(v):.3f})" for n, v in times.items()) +
-            f"  tiled==rows bitwise: {same}  cfg {qg.debug_config_tiled(M, N, K, wt)}", flush=True)
+            f"  tiled==rows bitwise: {same}  variants vs rows: {bits}  cfg {qg.debug_config_tiled(M, N, K, wt)}", flush=True)
         del copies, out
 
 
