@@ -24,7 +24,7 @@
 // The same configurations serve every weight layout (LAY_ROWS, LAY_TILED) and the activation-window
 // form (AW: odd K/32 against stage-padded weights).
 #pragma once
-#include "qg_mmq_kernel.hpp"
+#include "qg_mmql_kernel.hpp"
 
 namespace qg {
 
@@ -118,10 +118,38 @@ inline bool wide_rows(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.
 inline bool few_tiles(const GemmArgs& g) { return (long)((g.N + 31) / 32) * ((g.M + 31) / 32) <= device_cus(); }
 }  // namespace mmqd
 
+// Large M (qg_mmql_kernel.hpp): 64 rows x 64 tokens, 4 waves, two workgroups per CU, when that grid fills
+// the CUs twice over (>= 2 device_cus() tiles; 64 x 128 tiles with 8 waves measured 2-9 % slower:
+// profiles/r05_tuning/r5j_ab.txt, r5k_ab.txt); smaller grids keep the small tiles below. QG_MMQL=0 builds the round-4 dispatch
+// (A/B variant builds only); QG_MMQL_NBUF: shared stage buffers (a tuning choice, same bits).
+#ifndef QG_MMQL
+#define QG_MMQL 1
+#endif
+#ifndef QG_MMQL_NBUF
+#define QG_MMQL_NBUF 4
+#endif
+namespace mmqd {
+template <int F, int WR, int WC> bool mmql_ok(const GemmArgs& g) {
+    constexpr int NB = QG_MMQL_NBUF;
+    if (!QG_MMQL) return false;
+    // two workgroups per CU: at 1..1.5 per CU the small tiles are as fast or faster (r5l_ab.txt: M = 256
+    // 30.8 vs 23.6 us, M = 384 33.3 vs 33.3; M = 512 35.7 vs 43.1, M = 1024 67.6 vs 82.2)
+    if ((long)((g.N + 32 * WR - 1) / (32 * WR)) * ((g.M + 32 * WC - 1) / (32 * WC)) < 2L * device_cus()) return false;
+    return g.lay == LAY_TILED ? mmql_shape_ok<F, LAY_TILED, WR, WC, NB>(g) : mmql_shape_ok<F, LAY_ROWS, WR, WC, NB>(g);
+}
+template <int F, int WR, int WC> hipError_t mmql_run(const GemmArgs& g, hipStream_t st) {
+    constexpr int NB = QG_MMQL_NBUF;
+    if (g.lay == LAY_TILED)
+        return g.sumi ? mmql_launch<F, LAY_TILED, WR, WC, NB, true>(g, st) : mmql_launch<F, LAY_TILED, WR, WC, NB, false>(g, st);
+    return g.sumi ? mmql_launch<F, LAY_ROWS, WR, WC, NB, true>(g, st) : mmql_launch<F, LAY_ROWS, WR, WC, NB, false>(g, st);
+}
+}  // namespace mmqd
+
 // The configuration for the shape (above), or the 4-wave 32 x 32 tile where the preferred 8-wave one does
 // not fit the LDS with this layout (Q8_0 with activation windows).
 template <int F> int config(const GemmArgs& g) {
     using namespace mmqd;
+    if (g.M > 32 && mmql_ok<F, 2, 2>(g)) return 5;
     if (g.M <= 32) return wide_rows(g) ? (variant<F, 32, 1, 8>(g) ? 1 : 0) : (variant<F, 16, 1, 8>(g) ? 2 : 0);
     if (few_tiles(g) && variant<F, 32, 2, 8>(g)) return 3;
     return variant<F, 32, 2, 4>(g) ? 4 : 0;
@@ -136,6 +164,7 @@ template <int F> hipError_t launch_mfma_f(const GemmArgs& g, hipStream_t st) {
         case 2: return run_cfg<F, 16, 1, 8>(g, st);
         case 3: return run_cfg<F, 32, 2, 8>(g, st);
         case 4: return run_cfg<F, 32, 2, 4>(g, st);
+        case 5: return mmql_run<F, 2, 2>(g, st);
     }
     return hipErrorInvalidValue;
 }

@@ -173,7 +173,9 @@ def test_sumi_hook_runs_product_kernel(lib, m, n, k, t):
     prod = qg.debug_config(m, n, k, t)
     assert prod and prod == qg.debug_config(m, n, k, t, sumi=True)
     fam = {1: "gemv", 2: "mmq", 3: "generic", 4: "ragged"}[qg.select_algo(m, n, k, t)]
-    assert prod.startswith(fam + " ")
+    # the MFMA family: the small-tile kernel, or the large-M one (qg_mmql_kernel.hpp) when its grid fills
+    # the CUs
+    assert prod.startswith(fam + " ") or (fam == "mmq" and prod.startswith("mmql ")), prod
 
 
 def test_headline_configs_kernels(lib):
@@ -185,6 +187,10 @@ def test_headline_configs_kernels(lib):
     assert "BN=32 TT=1 W=12 P16=1 NB=1 LAY=0 AW=0" in qg.debug_config(32, 4096, 4096, 2)
     # the tiled layout of the same config: same tile, same waves
     assert "BN=32 TT=1 W=12 P16=1 NB=1 LAY=1 AW=0" in qg.debug_config_tiled(32, 4096, 4096, 2)
+    # the step-4 prefill (M = 512): the large-M kernel's 64 x 64 tiles (round 5), both layouts
+    assert qg.debug_config(512, 4096, 4096, 2).startswith("mmql F=2 BN=64 BM=64 W=4 NBUF=4 LAY=0 grid=512")
+    assert qg.debug_config_tiled(512, 4096, 4096, 2).startswith("mmql F=2 BN=64 BM=64 W=4 NBUF=4 LAY=1 grid=512")
+    assert qg.debug_config(256, 4096, 4096, 2).startswith("mmq F=2 ")  # 512 tiles of 64 x 64 needed
     for t in (3, 6, 7):
         assert qg.debug_config(1, 4096, 4096, t).startswith(f"gemv F={t} MT=1 ")
     assert qg.debug_config(1, 4000, 4096, 2).startswith("gemv F=2 MT=1 ")

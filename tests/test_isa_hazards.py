@@ -21,6 +21,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "llama.cpp-quant-gemm_amd", "quant_gemm", "libqg_hip.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 REQUIRED = 8
+# the 32 x 32 shapes (16 passes; the large-M prefill, qg_mmql_kernel.hpp) are held to 18, the CDNA3 ISA's
+# figure for a 16-pass XDL result read by VALU (not probed on gfx950: a margin, not a measurement)
+REQUIRED_32 = 18
 REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)(?!\w))")
 STOP = ("s_branch", "s_cbranch", "s_setpc", "s_endpgm", "s_barrier")
 
@@ -68,12 +71,14 @@ def instructions(listing):
 
 
 def test_mfma_results_padded(listing):
-    checked, violations, mfmas = 0, [], 0
+    checked, violations, mfmas, wide = 0, [], 0, []
     for fn, body in instructions(listing):
         for i, ins in enumerate(body):
             if not ins.startswith("v_mfma"):
                 continue
             mfmas += 1
+            if "_32x32x" in ins.split()[0]:
+                wide.append(ins.split()[0])
             ops = ins.split(None, 1)[1]
             dst = regs(ops.split(",")[0])
             states = 0
@@ -91,11 +96,13 @@ def test_mfma_results_padded(listing):
                             break
                     else:
                         checked += 1
-                        if states < REQUIRED:
+                        need = REQUIRED_32 if "_32x32x" in ins.split()[0] else REQUIRED
+                        if states < need:
                             violations.append(f"{fn}: {ins} -> {nxt} after {states} wait states")
                         break
                 m = re.match(r"s_nop\s+(\d+)", nxt)
                 states += int(m.group(1)) + 1 if m else 1
     assert mfmas > 100, "expected the prefill / W4A16 MFMA kernels in the library"
+    assert any("_32x32x" in f for f in wide), "expected the large-M prefill's 32 x 32 MFMAs"
     assert checked > mfmas // 4, (checked, mfmas)
     assert not violations, "\n".join(violations[:20])
