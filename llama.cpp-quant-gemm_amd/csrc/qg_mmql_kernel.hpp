@@ -69,6 +69,9 @@ template <int F, int LAY, int WR, int WC, int NBUF> struct mmql_geom {
     static_assert(TL || RSB % 16 == 0 || RSB % 16 == 8, "window shifts 0 / 8");
 };
 
+#ifndef QG_MMQL_PIPE
+#define QG_MMQL_PIPE 0
+#endif
 template <int F, int LAY, int WR, int WC, int NBUF, bool SUMI>
 __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, float* __restrict__ C,
                                           int32_t* __restrict__ sumi_out, int M, int N, int K, int ldc_m, int ldc_n) {
@@ -131,9 +134,12 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
     constexpr bool HAS_M = T::MOFF >= 0;
     constexpr bool HAS_S = F != FMT_Q8_0;
     constexpr float CFAC = F == FMT_Q4_0 ? -8.0f : F == FMT_Q5_0 ? -16.0f : 1.0f;
+    // the integer MFMA's seed: 1.5 * 2^23 (qg_mmq_kernel.hpp). Seeding 0 and converting with v_cvt_f32_i32
+    // instead of the v_sub measured 9 % slower (profiles/r05_tuning/mmql/r5n_ab.txt: M = 512 38.7 vs 35.4 us)
+    constexpr int SEED = MMQ_BIAS;
     i32x16 bias;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) bias[e] = MMQ_BIAS;
+    for (int e = 0; e < 16; ++e) bias[e] = SEED;
     float acc[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
@@ -155,7 +161,7 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int n = row_of(e);
-            if (n < N && m < M) sumi_out[((long)m * N + n) * nb + blk] = c[e] - MMQ_BIAS;
+            if (n < N && m < M) sumi_out[((long)m * N + n) * nb + blk] = c[e] - SEED;
         }
     };
 
@@ -280,6 +286,41 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
             ads[b] = adw(36 * b - 16 * (b == 0 ? 0 : 1));  // d_a | s_a, valid in half HB(b) (above)
         });
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (QG_MMQL_PIPE) {
+            // block-pipelined: block b's MFMAs issued before block b - 1's epilogue (2 blocks of results live)
+            if constexpr (HAS_S) {
+                const unsigned long xa = hh == 0 ? (unsigned long)(xw[0] & 0xFFFFu)
+                                                 : ((unsigned long)(xw[3] & 0xFFFFu) << 32) | (xw[2] << 16) | (xw[1] & 0xFFFFu);
+                const unsigned long sb = hh == 0 ? (unsigned long)(ads[0] >> 16)
+                                                 : ((unsigned long)(ads[3] >> 16) << 32) | (ads[2] & 0xFFFF0000u) | (ads[1] >> 16);
+                c2 = __builtin_amdgcn_mfma_f32_32x32x8f16(h4(xa), h4(sb), c2, 0, 0, 0);
+            }
+            f32x16 zz;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) zz[e] = 0.0f;
+            f32x16 pd[2];
+            i32x16 pc[2];
+            auto epi1 = [&](const f32x16& d1, const i32x16& c1, int blk) {
+                if constexpr (SUMI) {
+                    store_sumi(c1, blk);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[e] = __builtin_fmaf(d1[e], __int_as_float(c1[e]) - MMQ_BIAS_F, acc[e]);
+                }
+            };
+            static_for<MMQ_SB>([&](auto BI) {
+                constexpr int b = decltype(BI)::value;
+                const bool on = hh == (b == 0 ? 0 : 1);
+                pd[b & 1] = __builtin_amdgcn_mfma_f32_32x32x8f16(h4(on ? (unsigned long)(wdb[b] & 0xFFFFu) : 0ul),
+                                                                 h4(on ? (unsigned long)(ads[b] & 0xFFFFu) : 0ul), zz, 0, 0, 0);
+                pc[b & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[b], bfrag[b], bias, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (b > 0) epi1(pd[(b - 1) & 1], pc[(b - 1) & 1], h * MMQ_SB + b - 1);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            epi1(pd[1], pc[1], h * MMQ_SB + 3);
+            return;
+        }
         f32x16 dd[MMQ_SB];
         i32x16 cc[MMQ_SB];
         f32x16 z16;
@@ -333,10 +374,13 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
     }
 }
 
+#ifndef QG_MMQL_MINB
+#define QG_MMQL_MINB 2
+#endif
 // (A, B, M, N, K, out, ldc_m, ldc_n): 10 preloaded argument dwords; SUMI: out is the sumi hook's buffer.
 // One workgroup per CU (2 waves per SIMD at 8 waves): the accumulators and stage fragments take ~200 VGPRs.
 template <int F, int LAY, int WR, int WC, int NBUF, bool SUMI>
-__global__ __launch_bounds__(WR * WC * 64, WR * WC <= 4 ? 2 : 1) void mmql_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+__global__ __launch_bounds__(WR * WC * 64, WR * WC <= 4 ? QG_MMQL_MINB : 1) void mmql_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                int M, int N, int K, void* __restrict__ out, int ldc_m,
                                                                int ldc_n) {
     mmql_body<F, LAY, WR, WC, NBUF, SUMI>(A, B, SUMI ? nullptr : (float*)out, SUMI ? (int32_t*)out : nullptr, M, N, K, ldc_m,
