@@ -124,7 +124,8 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     (> 600 MB, so every launch streams from HBM) in a hipGraph, HIP events around the replays.
     forms: "single" (G launches), "batched" (one qg_gemm_w4a8_grouped launch over the G copies),
     "prepacked" / "padded" (the load-time padded layout), "tiled" (the load-time tiled layout,
-    qg_tile_weights + qg_gemm_w4a8_tiled), "w16" (qg_gemm_w4a16_ws: FP32 activations). Every row
+    qg_tile_weights + qg_gemm_w4a8_tiled), "tiled_act" (tiled weights and activations quantized into the tiled
+    activation layout, qg_quantize_q8_1_tiled + qg_gemm_w4a8_tiled_act), "w16" (qg_gemm_w4a16_ws: FP32 activations). Every row
     carries the NMSE vs an fp64 product of the unquantized inputs of ITS OWN form's output."""
     wt = WTYPES[wname]
     bb = qg.BLOCK_BYTES[wt]
@@ -139,11 +140,12 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
     ap = None
     if "padded" in forms:
         ap = qg.quantize_q8_1_padded(a)
+    at = qg.quantize_q8_1_tiled(a) if "tiled_act" in forms else None  # tiled activations (round 5)
     del b
     nbytes = algo_bytes(M, N, K, bb)
     res = []
     lib = qg._lib.load()
-    variant_of = {"prepacked": "repacked", "padded": "repacked", "tiled": "tiled"}
+    variant_of = {"prepacked": "repacked", "padded": "repacked", "tiled": "tiled", "tiled_act": "tiled"}
     copies, cur = None, None
     for form in forms:
         var = variant_of.get(form, "rows")
@@ -169,6 +171,13 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
                     if lib.qg_gemm_w4a8_tiled(P(aq.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N, K,
                                               wt, cs) != 0:
                         raise RuntimeError("qg_gemm_w4a8_tiled failed")
+        elif form == "tiled_act":
+            def step() -> None:
+                cs = P(torch.cuda.current_stream().cuda_stream)
+                for j in range(G):
+                    if lib.qg_gemm_w4a8_tiled_act(P(at.data_ptr()), P(copies[j].data_ptr()), P(out[j].data_ptr()), M, N,
+                                                  K, wt, cs) != 0:
+                        raise RuntimeError("qg_gemm_w4a8_tiled_act failed")
         elif form == "prepacked":
             wsb = lib.qg_gemm_w4a8_prepacked_workspace_size(M, K)
             ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
@@ -213,7 +222,7 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
         if label:
             row["label"] = label
         pub = REF_PUBLISHED.get((M, N, K))
-        if pub and form in ("single", "tiled") and wname == "q4_0":
+        if pub and form in ("single", "tiled", "tiled_act") and wname == "q4_0":
             row["ref_published_gflops"], row["ref_source"] = pub
             row["vs_ref_published"] = round(tops * 1e3 / pub[0], 2)
         if M >= 128 and form != "w16":
@@ -936,14 +945,14 @@ def main() -> None:
             # of G: the denominators of the N>1 strong-scaling ratios
             del mods, wcopies
             torch.cuda.empty_cache()
-            sides = [("q4_0", 32, 4096, 4096, ("single", "tiled"), "configs[2]"),
+            sides = [("q4_0", 32, 4096, 4096, ("single", "tiled", "tiled_act"), "configs[2]"),
                      ("q4_0", 1, 4096, 4096, ("tiled",), "configs[1] on the tiled layout (decode GEMV)"),
                      ("q4_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q5_0", 1, 4096, 4096, ("single",), "configs[3]"), ("q5_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q4_0", 1, 32000, 4096, ("single", "batched"), "configs[4] on one GPU"),
                      # odd K/32 at a prefill size: the load-time padded layout and the
                      # tiled layout (round 5)
-                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded", "tiled"), "odd K/32"),
+                     ("q4_0", 32, 4096, 4128, ("prepacked", "padded", "tiled", "tiled_act"), "odd K/32"),
                      # row f3: the W4A16 prefill (FP32 activations x Q4_0), M = 32
                      ("q4_0", 32, 4096, 4096, ("w16",), "row f3"),
                      # the reference's published shapes: 2D-tile table
@@ -958,7 +967,7 @@ def main() -> None:
                      ("q4_0", 8, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
                      ("q4_0", 2, 8192, 14336, ("single",), "published 8192x2x14336"),
                      ("q4_0", 128, 4096, 4096, ("single", "tiled"), "step4 prefill"),
-                     ("q4_0", 512, 4096, 4096, ("single", "tiled"), "step4 prefill (published ~2.7 TFLOPS)"),
+                     ("q4_0", 512, 4096, 4096, ("single", "tiled", "tiled_act"), "step4 prefill (published ~2.7 TFLOPS)"),
                      ("q4_0", 512, 4096, 14336, ("single", "tiled"), "step4 prefill")]
             out["side_configs"] = [r for (w, m_, n_, k_, f, lab) in sides
                                    for r in measure_config(w, m_, n_, k_, dev, forms=f, label=lab)]

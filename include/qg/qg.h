@@ -147,6 +147,27 @@ int qg_debug_sumi_tiled(const void* A_q8_1, const void* B_tiled, int32_t* sumi, 
                         qg_stream_t stream);
 int qg_debug_config_tiled(int M, int N, int K, int wtype, int sumi, char* buf, size_t len);
 
+/* TILED ACTIVATIONS (round 5) — the activation side of the tiled layout, for the prefill on tiled weights:
+ * tokens in tiles of 16, K/32 in stages of 4 blocks, each (token tile, stage) one contiguous run of 2304 bytes
+ * holding the 16 tokens' 4 block_q8_1 (token-major: token t's blocks at t * 144 + j * 36); tiles follow each
+ * other tile-major, stages within a tile in order; tokens past M (to a multiple of 16) and blocks past K/32 (to
+ * a multiple of 4) are zero blocks. qg_activations_tiled_bytes(M, K) sizes it. qg_quantize_q8_1_tiled writes it
+ * straight from FP32 rows (16-B aligned x and A_tiled; each real block's bytes are qg_quantize_q8_1's);
+ * qg_tile_activations rearranges existing Q8_1 rows into it. qg_gemm_w4a8_tiled_act(A_tiled, B_tiled, ...)
+ * then computes the same product as qg_gemm_w4a8_tiled(A_q8_1, B_tiled, ...) (the same kernels and tile
+ * configurations, so the same bits) with every stage of BOTH operands one linear DMA stream. _ldc, the parity
+ * hook and the configuration query as for qg_gemm_w4a8_tiled. */
+size_t qg_activations_tiled_bytes(int M, int K);
+int qg_quantize_q8_1_tiled(const float* x, void* A_tiled, int M, int K, qg_stream_t stream);
+int qg_tile_activations(const void* A_q8_1, void* A_tiled, int M, int K, qg_stream_t stream);
+int qg_gemm_w4a8_tiled_act(const void* A_tiled, const void* B_tiled, float* C, int M, int N, int K, int wtype,
+                           qg_stream_t stream);
+int qg_gemm_w4a8_tiled_act_ldc(const void* A_tiled, const void* B_tiled, float* C, int M, int N, int K, int64_t ldc,
+                               int wtype, qg_stream_t stream);
+int qg_debug_sumi_tiled_act(const void* A_tiled, const void* B_tiled, int32_t* sumi, int M, int N, int K, int wtype,
+                            qg_stream_t stream);
+int qg_debug_config_tiled_act(int M, int N, int K, int wtype, int sumi, char* buf, size_t len);
+
 /* W8A8: Q8_0 weights x Q8_1 activations, term sumi * d_a * d_w. Replaces gemm_w8a8_{naive,dp4a}
  * (include/gemm_cuda_naive.cuh:294-301, gemm_cuda_dp4a.cuh:418-425); device twin of
  * gemm_w8a8_reference (include/gemm_reference.h:233-267). Same as qg_gemm_w4a8(..., QG_TYPE_Q8_0). */

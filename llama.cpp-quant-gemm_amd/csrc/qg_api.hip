@@ -564,6 +564,67 @@ int qg_debug_config_tiled(int M, int N, int K, int wtype, int sumi, char* buf, s
     return run_tiled(g, nullptr);
 }
 
+// ---- round 5: tiled activations (LAY_TILED_ACT) -------------------------------------------------------
+size_t qg_activations_tiled_bytes(int M, int K) {
+    if (M < 0 || K <= 0 || K % 32 != 0) return 0;
+    return tiled_act_bytes(M, K);
+}
+
+int qg_quantize_q8_1_tiled(const float* x, void* A_tiled, int M, int K, qg_stream_t stream) {
+    if (M < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (M == 0) return QG_OK;
+    if (!x || !A_tiled) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)x & 15) != 0 || ((uintptr_t)A_tiled & 15) != 0) return QG_ERR_ALIGN;
+    return hip_status(launch_quantize_q8_1_tiled(x, A_tiled, M, K, (hipStream_t)stream));
+}
+
+int qg_tile_activations(const void* A_q8_1, void* A_tiled, int M, int K, qg_stream_t stream) {
+    if (M < 0) return QG_ERR_INVALID_ARG;
+    if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;
+    if (M == 0) return QG_OK;
+    if (!A_q8_1 || !A_tiled) return QG_ERR_INVALID_ARG;
+    if (((uintptr_t)A_q8_1 & 3) != 0 || ((uintptr_t)A_tiled & 15) != 0) return QG_ERR_ALIGN;
+    return hip_status(launch_tile_activations(A_q8_1, A_tiled, M, K, (hipStream_t)stream));
+}
+
+int qg_gemm_w4a8_tiled_act_ldc(const void* A_tiled, const void* B_tiled, float* C, int M, int N, int K, int64_t ldc, int wtype,
+                               qg_stream_t stream) {
+    if (ldc < N || (M > 1 && ldc <= 0)) return QG_ERR_INVALID_ARG;
+    GemmArgs g;
+    g.A = A_tiled; g.B = B_tiled; g.C = C; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = (long)ldc; g.ldc_n = 1;
+    g.lay = LAY_TILED_ACT;
+    return run_tiled(g, (hipStream_t)stream);
+}
+
+int qg_gemm_w4a8_tiled_act(const void* A_tiled, const void* B_tiled, float* C, int M, int N, int K, int wtype,
+                           qg_stream_t stream) {
+    return qg_gemm_w4a8_tiled_act_ldc(A_tiled, B_tiled, C, M, N, K, N, wtype, stream);
+}
+
+int qg_debug_sumi_tiled_act(const void* A_tiled, const void* B_tiled, int32_t* sumi, int M, int N, int K, int wtype,
+                            qg_stream_t stream) {
+    GemmArgs g;
+    g.A = A_tiled; g.B = B_tiled; g.sumi = sumi; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.lay = LAY_TILED_ACT;
+    return run_tiled(g, (hipStream_t)stream);
+}
+
+int qg_debug_config_tiled_act(int M, int N, int K, int wtype, int sumi, char* buf, size_t len) {
+    if (!buf || len == 0) return QG_ERR_INVALID_ARG;
+    buf[0] = 0;
+    GemmArgs g;
+    g.A = (const void*)256; g.B = (const void*)256; g.M = M; g.N = N; g.K = K; g.wtype = wtype;
+    if (sumi) g.sumi = (int32_t*)256;
+    else g.C = (float*)256;
+    g.ldc_m = N; g.ldc_n = 1;
+    g.lay = LAY_TILED_ACT;
+    g.describe = buf; g.describe_len = len;
+    return run_tiled(g, nullptr);
+}
+
 int qg_gemm_w4a8_grouped(const qg_gemv_item* items, int count, int M, int K, int wtype, qg_stream_t stream) {
     if (count < 0 || M < 0 || (count > 0 && !items)) return QG_ERR_INVALID_ARG;
     if (K <= 0 || K % 32 != 0) return QG_ERR_BAD_K;

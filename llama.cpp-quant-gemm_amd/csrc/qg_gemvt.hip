@@ -26,7 +26,7 @@ constexpr int GT_W = 16;  // waves per workgroup (16 rows)
 
 template <int CTRL> __device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
 
-template <int F, int MT, bool SUMI>
+template <int F, int MT, bool SUMI, bool TA>
 __global__ __launch_bounds__(GT_W * 64) void gemvt_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, int M, int N,
                                                          int K, void* __restrict__ out, int ldc_m, int ldc_n) {
     using T = wfmt<F>;
@@ -66,8 +66,13 @@ __global__ __launch_bounds__(GT_W * 64) void gemvt_kernel(const uint8_t* __restr
     uint32_t ab[9];
     const uint32_t* A32 = reinterpret_cast<const uint32_t*>(A);
     auto load_ablk = [&](int g) {
+        long src = (long)g * 9;
+        if constexpr (TA) {  // LAY_TILED_ACT: block b of token m inside its tile's 2304-B stage run
+            const int m = g / nb, b = g - m * nb;
+            src = (((long)(m / ACT_TILE) * H + b / MMQ_SB) * ACT_TILE + m % ACT_TILE) * (MMQ_SB * 9) + (b % MMQ_SB) * 9;
+        }
 #pragma unroll
-        for (int i = 0; i < 9; ++i) ab[i] = A32[(long)g * 9 + i];
+        for (int i = 0; i < 9; ++i) ab[i] = A32[src + i];
     };
     if (tid < totb) load_ablk(tid);
     // every stage of this wave (up to NS) in flight before the staging barrier; beyond NS (K > 8192) one
@@ -178,13 +183,15 @@ template <int F, int MT> hipError_t gemvt_launch(const GemmArgs& g, hipStream_t 
     const int grid = (g.N + 15) / 16;
     const size_t lds = std::max((size_t)g.M * (g.K / QK) * 36, (size_t)MT * GT_W * 16 * 4);
     if (g.describe) {
-        describe_kernel(g, "gemvt F=%d MT=%d W=%d grid=%d", F, MT, GT_W, grid);
+        describe_kernel(g, "gemvt F=%d MT=%d W=%d TA=%d grid=%d", F, MT, GT_W, (int)(g.lay == LAY_TILED_ACT), grid);
         return hipSuccess;
     }
-    auto k = g.sumi ? gemvt_kernel<F, MT, true> : gemvt_kernel<F, MT, false>;
+    const bool ta = g.lay == LAY_TILED_ACT;
+    auto k = g.sumi ? (ta ? gemvt_kernel<F, MT, true, true> : gemvt_kernel<F, MT, true, false>)
+                    : (ta ? gemvt_kernel<F, MT, false, true> : gemvt_kernel<F, MT, false, false>);
     if (lds > 64 * 1024) {
-        static std::atomic<unsigned long long> done[2] = {};
-        const hipError_t e = set_max_lds_once((const void*)k, 160 * 1024, done[g.sumi ? 1 : 0]);
+        static std::atomic<unsigned long long> done[4] = {};
+        const hipError_t e = set_max_lds_once((const void*)k, 160 * 1024, done[(g.sumi ? 1 : 0) + (ta ? 2 : 0)]);
         if (e != hipSuccess) return e;
     }
     void* out = g.sumi ? (void*)g.sumi : (void*)g.C;
@@ -208,7 +215,7 @@ template <int F> hipError_t gemvt_f(const GemmArgs& g, hipStream_t st) {
 // per-token LDS reads and quad reductions grow with M), so M = 2..4 run the MFMA kernel. The activation
 // row within the LDS, 32-bit strides (A 4-B aligned, B_tiled 16-B aligned).
 bool gemvt_eligible(const GemmArgs& g) {
-    return g.lay == LAY_TILED && g.M == 1 && g.N >= 1 && g.K % QK == 0 && ((uintptr_t)g.B & 15) == 0 &&
+    return (g.lay == LAY_TILED || g.lay == LAY_TILED_ACT) && g.M == 1 && g.N >= 1 && g.K % QK == 0 && ((uintptr_t)g.B & 15) == 0 &&
            ((uintptr_t)g.A & 3) == 0 && (size_t)g.M * (g.K / QK) * 36 <= 144 * 1024 && g.ldc_m <= INT32_MAX &&
            g.ldc_n <= INT32_MAX && (long)g.M * g.N * (g.K / QK) < (1L << 62);
 }

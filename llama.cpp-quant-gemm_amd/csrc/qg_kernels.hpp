@@ -12,7 +12,11 @@ namespace qg {
 enum : int { AIN_Q8_1 = 0, AIN_F32 = 1, AIN_F16_FUSED = 2 };
 
 // Weight layouts of the MFMA kernel (qg_mmq_kernel.hpp): the reference's rows, or qg_tile_weights' tiles.
-enum : int { LAY_ROWS = 0, LAY_TILED = 1 };
+// LAY_TILED_ACT: tiled weights AND tiled activations (qg_quantize_q8_1_tiled: 16-token tiles, 4-block stages,
+// each (token tile, stage) one contiguous 2304-B run of the 16 tokens' 144-B stage segments, zero padded)
+enum : int { LAY_ROWS = 0, LAY_TILED = 1, LAY_TILED_ACT = 2 };
+constexpr int ACT_TILE = 16;                              // tokens per activation tile (LAY_TILED_ACT)
+constexpr int ACT_STG = ACT_TILE * 4 * 36;                // bytes per (token tile, stage): 2304
 
 // One W4A8 product C = A_q8_1 * B_w^T, activation-major indices (m = activation row, n = weight
 // row); the output element (m, n) lives at C[m * ldc_m + n * ldc_n].
@@ -140,6 +144,10 @@ hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64
 hipError_t launch_quantize_f16_fused(const void* x, void* y, int64_t nblocks, hipStream_t st);
 // FP32 rows of nb blocks -> Q8_1 rows of nbp blocks, zero blocks after the real ones.
 hipError_t launch_quantize_q8_1_padded(const float* x, void* y, int64_t rows, int nb, int nbp, hipStream_t st);
+// the tiled activation layout (LAY_TILED_ACT): its size, the quantizer writing it, the Q8_1-row repack into it
+size_t tiled_act_bytes(int M, int K);
+hipError_t launch_quantize_q8_1_tiled(const float* x, void* y, int M, int K, hipStream_t st);
+hipError_t launch_tile_activations(const void* a, void* y, int M, int K, hipStream_t st);
 hipError_t launch_dequantize(int type, const void* x, float* y, int64_t nblocks, hipStream_t st);
 
 }  // namespace qg

@@ -54,9 +54,9 @@ template <int BN, int TT, int W> constexpr bool short_sig = (BN == 16 && W == 8)
 #define QG_MMQ_TILED_NB 1
 #endif
 template <int F, int BN, int TT, int LAY>
-constexpr int alt_w = BN == 32 && TT == 1 ? (LAY == LAY_TILED ? QG_MMQ_TILED_W : 12) : BN == 16 ? (F != FMT_Q8_0 ? 16 : 8) : 8;
+constexpr int alt_w = BN == 32 && TT == 1 ? (LAY != LAY_ROWS ? QG_MMQ_TILED_W : 12) : BN == 16 ? (F != FMT_Q8_0 ? 16 : 8) : 8;
 template <int F, int BN, int TT, int LAY>
-constexpr int alt_nb = BN == 32 && TT == 1 ? (LAY == LAY_TILED ? QG_MMQ_TILED_NB : 1) : BN == 16 ? (F != FMT_Q8_0 ? 1 : 2) : 2;
+constexpr int alt_nb = BN == 32 && TT == 1 ? (LAY != LAY_ROWS ? QG_MMQ_TILED_NB : 1) : BN == 16 ? (F != FMT_Q8_0 ? 1 : 2) : 2;
 
 // grid of one dispatch round: at most one workgroup per CU (device_cus(): 256 on a whole MI355X)
 inline bool one_round(const GemmArgs& g, int BN, int NTOK) {
@@ -84,6 +84,7 @@ template <int F, int BN, int TT, int W, bool P16, int LAY, bool AW> hipError_t r
 // == 0 and B is 16-B aligned (else 4-B pieces), the activation-window form for the prepacked rows
 // (g.nbw); LAY_TILED with or without activation windows.
 template <int F, int BN, int TT, int W> int variant(const GemmArgs& g) {
+    if (g.lay == LAY_TILED_ACT) return mmq_shape_ok<F, BN, TT, W, true, 2, LAY_TILED_ACT, false>(g) ? 6 : 0;
     if (g.lay == LAY_TILED) {
         if (mmq_shape_ok<F, BN, TT, W, true, 2, LAY_TILED, false>(g)) return 3;
         if (mmq_shape_ok<F, BN, TT, W, true, 2, LAY_TILED, true>(g)) return 4;
@@ -107,6 +108,7 @@ template <int F, int BN, int TT, int W> hipError_t run_cfg(const GemmArgs& g, hi
         case 3: return run_fit<F, BN, TT, W, true, LAY_TILED, false>(g, st);
         case 4: return run_fit<F, BN, TT, W, true, LAY_TILED, true>(g, st);
         case 5: return run_fit<F, BN, TT, W, true, LAY_ROWS, true>(g, st);
+        case 6: return run_fit<F, BN, TT, W, true, LAY_TILED_ACT, false>(g, st);
     }
     return hipErrorInvalidValue;
 }
@@ -135,10 +137,13 @@ template <int F, int WR, int WC> bool mmql_ok(const GemmArgs& g) {
     // two workgroups per CU: at 1..1.5 per CU the small tiles are as fast or faster (r5l_ab.txt: M = 256
     // 30.8 vs 23.6 us, M = 384 33.3 vs 33.3; M = 512 35.7 vs 43.1, M = 1024 67.6 vs 82.2)
     if ((long)((g.N + 32 * WR - 1) / (32 * WR)) * ((g.M + 32 * WC - 1) / (32 * WC)) < 2L * device_cus()) return false;
+    if (g.lay == LAY_TILED_ACT) return mmql_shape_ok<F, LAY_TILED_ACT, WR, WC, NB>(g);
     return g.lay == LAY_TILED ? mmql_shape_ok<F, LAY_TILED, WR, WC, NB>(g) : mmql_shape_ok<F, LAY_ROWS, WR, WC, NB>(g);
 }
 template <int F, int WR, int WC> hipError_t mmql_run(const GemmArgs& g, hipStream_t st) {
     constexpr int NB = QG_MMQL_NBUF;
+    if (g.lay == LAY_TILED_ACT)
+        return g.sumi ? mmql_launch<F, LAY_TILED_ACT, WR, WC, NB, true>(g, st) : mmql_launch<F, LAY_TILED_ACT, WR, WC, NB, false>(g, st);
     if (g.lay == LAY_TILED)
         return g.sumi ? mmql_launch<F, LAY_TILED, WR, WC, NB, true>(g, st) : mmql_launch<F, LAY_TILED, WR, WC, NB, false>(g, st);
     return g.sumi ? mmql_launch<F, LAY_ROWS, WR, WC, NB, true>(g, st) : mmql_launch<F, LAY_ROWS, WR, WC, NB, false>(g, st);

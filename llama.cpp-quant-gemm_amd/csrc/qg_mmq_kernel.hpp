@@ -123,7 +123,8 @@ template <int SZ> __device__ __forceinline__ void glds(const uint8_t* g, uint8_t
 template <int F, int BN, int TT, int W, bool P16, int NB, int LAY, bool AW> struct mmq_geom {
     using T = wfmt<F>;
     using TF = tiled_fmt<F>;
-    static constexpr bool TL = LAY == LAY_TILED;
+    static constexpr bool TL = LAY != LAY_ROWS;               // tiled weights (LAY_TILED, LAY_TILED_ACT)
+    static constexpr bool TA = LAY == LAY_TILED_ACT;          // tiled activations
     static constexpr int RSB = MMQ_SB * T::BB;                 // weight bytes per row per stage
     static constexpr int WPS = (P16 || TL) ? 16 : 4;           // weight DMA piece (bytes)
     static constexpr int RIMG = TL ? RSB : P16 && RSB % 16 != 0 ? RSB + 8 : RSB;  // LAY_ROWS row image bytes
@@ -189,7 +190,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     const int m0 = blockIdx.y * G::NTOK;
     const int nb = K / QK;
     const int H = nb / MMQ_SB;  // stages
-    if constexpr (!AW) nba = nb;
+    if constexpr (!AW && LAY != LAY_TILED_ACT) nba = nb;  // (tiled activations: nba = the real blocks, sumi hook)
     const long RB = (long)nb * T::BB;
     const long AB = (long)nba * Q8_1_BYTES;
     uint8_t* bufs = smem + wave * NB * G::BUF;
@@ -200,7 +201,10 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     // address correctly and the per-lane offsets stay small (mmq_shape_ok)
     const int r0 = TL ? n0 % TILE_ROWS : 0;  // LAY_TILED: the workgroup's first row within its tile
     const uint8_t* Bw = TL ? B + (long)(n0 / TILE_ROWS) * H * TF::STG : B + (long)n0 * RB;
-    const uint8_t* Aw = A + (long)m0 * AB;
+    // tiled activations: the workgroup's first 16-token tile (m0 is a multiple of 16); tiles past the last
+    // one (TT = 2 at M % 32 in 1..16) read the last tile, their outputs are dropped
+    const int nat = (M + ACT_TILE - 1) / ACT_TILE;
+    const uint8_t* Aw = G::TA ? A + (long)(m0 / ACT_TILE) * H * ACT_STG : A + (long)m0 * AB;
     auto wpiece = [&](int p) {  // weight piece p of a stage: byte offset from the stage's base
         if constexpr (TL) {
             const int o = 16 * p;  // the image's planes, each a contiguous run of the tile's stage
@@ -214,6 +218,10 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     };
     auto apiece = [&](int p) {  // activation piece p of a stage: byte offset from Aw (+ the stage's)
         const int tok = p / G::APT;
+        if constexpr (G::TA) {  // the token's 144-B segment inside its tile's 2304-B stage run
+            const int sub = min(m0 / ACT_TILE + tok / ACT_TILE, nat - 1) - m0 / ACT_TILE;
+            return sub * H * ACT_STG + (tok % ACT_TILE) * (MMQ_SB * Q8_1_BYTES) + (p - tok * G::APT) * 16;
+        }
         const int t0 = (min(m0 + tok, M - 1) - m0) * (int)AB;
         const int j = min(p - tok * G::APT, G::APR - 1);
         if constexpr (AW) return t0 - (t0 & 15) + j * 16;  // the 16-B aligned window around the segment
@@ -245,7 +253,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     // (found by tools/archive/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = TL ? Bw + (long)h * TF::STG : Bw + (long)h * G::RSB - G::shift(h);
-        const uint8_t* asrc = Aw + (long)h * (MMQ_SB * Q8_1_BYTES);
+        const uint8_t* asrc = Aw + (long)h * (G::TA ? ACT_STG : MMQ_SB * Q8_1_BYTES);
         if constexpr (G::CMB) {
 #pragma unroll
             for (int i = 0; i < G::NI; ++i) glds<16>((cisw[i] ? wsrc : asrc) + coff[i], buf + 64 * i * 16);
@@ -556,7 +564,7 @@ __global__ __launch_bounds__(W * 64, W <= 4 ? 2 : 1) void mmqt_kernel(const uint
 // g.K is the logical K; LAY_TILED and AW run on the weight side's K (mmq_weight_k).
 inline int mmq_weight_k(const GemmArgs& g) {
     const int nb = g.K / QK;
-    if (g.lay == LAY_TILED) return (nb + MMQ_SB - 1) / MMQ_SB * MMQ_SB * QK;
+    if (g.lay != LAY_ROWS) return (nb + MMQ_SB - 1) / MMQ_SB * MMQ_SB * QK;
     return g.nbw > 0 ? g.nbw * QK : g.K;
 }
 template <int F, int BN, int TT, int W, bool P16, int NB = 2, int LAY = LAY_ROWS, bool AW = false>
@@ -565,9 +573,11 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
     if (!G::FITS) return false;
     const int K = mmq_weight_k(g), nba = g.K / QK;
     if (g.M < 1 || g.N < 1 || g.K % QK != 0 || K % (QK * MMQ_SB) != 0 || K < g.K) return false;
-    if (AW != (nba % MMQ_SB != 0 || K != g.K)) return false;  // windows exactly when the rows differ
-    if (LAY == LAY_TILED) {
-        if (g.lay != LAY_TILED || ((uintptr_t)g.B & 15) != 0) return false;
+    if (LAY == LAY_TILED_ACT) {
+        if (AW) return false;  // the tiled activations are zero padded to whole stages
+    } else if (AW != (nba % MMQ_SB != 0 || K != g.K)) return false;  // windows exactly when the rows differ
+    if (LAY != LAY_ROWS) {
+        if (g.lay != LAY || ((uintptr_t)g.B & 15) != 0) return false;
         if ((long)tiled_fmt<F>::STG * (K / QK / MMQ_SB) >= (1L << 31)) return false;
     } else {
         if (g.lay != LAY_ROWS) return false;
@@ -577,8 +587,13 @@ inline bool mmq_shape_ok(const GemmArgs& g) {
         if (RB * BN >= (1L << 31)) return false;  // per-lane DMA offsets are 32-bit
     }
     const long AB = (long)nba * Q8_1_BYTES;
-    if (((uintptr_t)g.A & 15) != 0 || (!AW && AB % 16 != 0)) return false;
-    if (AB * G::NTOK >= (1L << 31) || (AW && AB * g.M >= (1L << 31))) return false;
+    if (LAY == LAY_TILED_ACT) {
+        if (((uintptr_t)g.A & 15) != 0 || (long)ACT_STG * (K / QK / MMQ_SB) * ((G::NTOK + ACT_TILE - 1) / ACT_TILE) >= (1L << 31))
+            return false;
+    } else {
+        if (((uintptr_t)g.A & 15) != 0 || (!AW && AB % 16 != 0)) return false;
+        if (AB * G::NTOK >= (1L << 31) || (AW && AB * g.M >= (1L << 31))) return false;
+    }
     if (g.ldc_m > INT32_MAX || g.ldc_n > INT32_MAX) return false;  // the short entries' 32-bit strides
     return true;
 }

@@ -44,7 +44,8 @@ namespace qg {
 template <int F, int LAY, int WR, int WC, int NBUF> struct mmql_geom {
     using T = wfmt<F>;
     using TF = tiled_fmt<F>;
-    static constexpr bool TL = LAY == LAY_TILED;
+    static constexpr bool TL = LAY != LAY_ROWS;
+    static constexpr bool TA = LAY == LAY_TILED_ACT;
     static constexpr int W = WR * WC, BN = 32 * WR, BM = 32 * WC;
     static constexpr int RSB = MMQ_SB * T::BB;                         // weight bytes per row per stage
     static constexpr int RIMG = RSB % 16 != 0 ? RSB + 8 : RSB;         // LAY_ROWS 16-B aligned row window
@@ -69,9 +70,6 @@ template <int F, int LAY, int WR, int WC, int NBUF> struct mmql_geom {
     static_assert(TL || RSB % 16 == 0 || RSB % 16 == 8, "window shifts 0 / 8");
 };
 
-#ifndef QG_MMQL_PIPE
-#define QG_MMQL_PIPE 0
-#endif
 template <int F, int LAY, int WR, int WC, int NBUF, bool SUMI>
 __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B, float* __restrict__ C,
                                           int32_t* __restrict__ sumi_out, int M, int N, int K, int ldc_m, int ldc_n) {
@@ -98,7 +96,8 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
 
     const int ntl = (N + TILE_ROWS - 1) / TILE_ROWS;  // LAY_TILED tiles
     const uint8_t* Bw = TL ? B + (long)(n0 / TILE_ROWS) * H * TF::STG : B + (long)n0 * RB;
-    const uint8_t* Aw = A + (long)m0 * AB;
+    const int nat = (M + ACT_TILE - 1) / ACT_TILE;  // tiled activations: 16-token tiles
+    const uint8_t* Aw = G::TA ? A + (long)(m0 / ACT_TILE) * H * ACT_STG : A + (long)m0 * AB;
     // per-lane piece offsets (bytes from Bw / Aw, before the stage's) of wave-instruction gi = i W + wave
     int off[G::NI];
     bool isw[G::NI];  // wave-uniform
@@ -118,12 +117,17 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
             }
         } else {
             const int pa = min(64 * (gi - G::PWI) + lane, G::PA - 1), tok = pa / G::APT;
-            off[i] = (min(m0 + tok, M - 1) - m0) * (int)AB + (pa - tok * G::APT) * 16;
+            if constexpr (G::TA) {
+                const int sub = min(m0 / ACT_TILE + tok / ACT_TILE, nat - 1) - m0 / ACT_TILE;
+                off[i] = sub * H * ACT_STG + (tok % ACT_TILE) * (MMQ_SB * Q8_1_BYTES) + (pa - tok * G::APT) * 16;
+            } else {
+                off[i] = (min(m0 + tok, M - 1) - m0) * (int)AB + (pa - tok * G::APT) * 16;
+            }
         }
     }
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = TL ? Bw + (long)h * TF::STG : Bw + (long)h * G::RSB - G::shift(h);
-        const uint8_t* asrc = Aw + (long)h * (MMQ_SB * Q8_1_BYTES);
+        const uint8_t* asrc = Aw + (long)h * (G::TA ? ACT_STG : MMQ_SB * Q8_1_BYTES);
 #pragma unroll
         for (int i = 0; i < G::NI; ++i) glds<16>((isw[i] ? wsrc : asrc) + off[i], buf + 64 * (i * G::W + wave) * 16);
     };
@@ -286,41 +290,6 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
             ads[b] = adw(36 * b - 16 * (b == 0 ? 0 : 1));  // d_a | s_a, valid in half HB(b) (above)
         });
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (QG_MMQL_PIPE) {
-            // block-pipelined: block b's MFMAs issued before block b - 1's epilogue (2 blocks of results live)
-            if constexpr (HAS_S) {
-                const unsigned long xa = hh == 0 ? (unsigned long)(xw[0] & 0xFFFFu)
-                                                 : ((unsigned long)(xw[3] & 0xFFFFu) << 32) | (xw[2] << 16) | (xw[1] & 0xFFFFu);
-                const unsigned long sb = hh == 0 ? (unsigned long)(ads[0] >> 16)
-                                                 : ((unsigned long)(ads[3] >> 16) << 32) | (ads[2] & 0xFFFF0000u) | (ads[1] >> 16);
-                c2 = __builtin_amdgcn_mfma_f32_32x32x8f16(h4(xa), h4(sb), c2, 0, 0, 0);
-            }
-            f32x16 zz;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) zz[e] = 0.0f;
-            f32x16 pd[2];
-            i32x16 pc[2];
-            auto epi1 = [&](const f32x16& d1, const i32x16& c1, int blk) {
-                if constexpr (SUMI) {
-                    store_sumi(c1, blk);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[e] = __builtin_fmaf(d1[e], __int_as_float(c1[e]) - MMQ_BIAS_F, acc[e]);
-                }
-            };
-            static_for<MMQ_SB>([&](auto BI) {
-                constexpr int b = decltype(BI)::value;
-                const bool on = hh == (b == 0 ? 0 : 1);
-                pd[b & 1] = __builtin_amdgcn_mfma_f32_32x32x8f16(h4(on ? (unsigned long)(wdb[b] & 0xFFFFu) : 0ul),
-                                                                 h4(on ? (unsigned long)(ads[b] & 0xFFFFu) : 0ul), zz, 0, 0, 0);
-                pc[b & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(afrag[b], bfrag[b], bias, 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (b > 0) epi1(pd[(b - 1) & 1], pc[(b - 1) & 1], h * MMQ_SB + b - 1);
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            epi1(pd[1], pc[1], h * MMQ_SB + 3);
-            return;
-        }
         f32x16 dd[MMQ_SB];
         i32x16 cc[MMQ_SB];
         f32x16 z16;
@@ -374,13 +343,10 @@ __device__ __forceinline__ void mmql_body(const uint8_t* __restrict__ A, const u
     }
 }
 
-#ifndef QG_MMQL_MINB
-#define QG_MMQL_MINB 2
-#endif
 // (A, B, M, N, K, out, ldc_m, ldc_n): 10 preloaded argument dwords; SUMI: out is the sumi hook's buffer.
 // One workgroup per CU (2 waves per SIMD at 8 waves): the accumulators and stage fragments take ~200 VGPRs.
 template <int F, int LAY, int WR, int WC, int NBUF, bool SUMI>
-__global__ __launch_bounds__(WR * WC * 64, WR * WC <= 4 ? QG_MMQL_MINB : 1) void mmql_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+__global__ __launch_bounds__(WR * WC * 64, WR * WC <= 4 ? 2 : 1) void mmql_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                int M, int N, int K, void* __restrict__ out, int ldc_m,
                                                                int ldc_n) {
     mmql_body<F, LAY, WR, WC, NBUF, SUMI>(A, B, SUMI ? nullptr : (float*)out, SUMI ? (int32_t*)out : nullptr, M, N, K, ldc_m,
@@ -396,8 +362,9 @@ template <int F, int LAY, int WR, int WC, int NBUF> inline bool mmql_shape_ok(co
     if (g.M < 1 || g.N < 1 || g.K % (QK * MMQ_SB) != 0) return false;
     if (((uintptr_t)g.A & 15) != 0 || ((uintptr_t)g.B & 15) != 0) return false;
     const long nb = g.K / QK, AB = nb * Q8_1_BYTES;
-    if (LAY == LAY_TILED) {
+    if (LAY != LAY_ROWS) {
         if ((long)tiled_fmt<F>::STG * (nb / MMQ_SB) * WR >= (1L << 31)) return false;
+        if (LAY == LAY_TILED_ACT && (long)ACT_STG * (nb / MMQ_SB) * (G::BM / ACT_TILE) >= (1L << 31)) return false;
     } else {
         const long RB = nb * wfmt<F>::BB;
         if (RB % 16 != 0 || (G::RSB % 16 != 0 && g.K % 256 != 0)) return false;

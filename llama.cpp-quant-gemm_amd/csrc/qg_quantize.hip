@@ -202,14 +202,9 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 //     what lane j - 1 handed over by DPP row_shr:1), the very sequence of fp32 adds of the reference loop;
 //   variant 1: s = d * sum(q) (an integer sum, any order).
 // Lane j stores qs dword j; lane 7 (which ends holding s) stores the d | s dword.
-template <int VARIANT>
-__global__ __launch_bounds__(64) void quantize_q8_1_lanes_kernel(const float4* __restrict__ x, uint32_t* __restrict__ y,
-                                                                 int64_t nblocks) {
-    const int64_t gi = (int64_t)blockIdx.x * 64 + threadIdx.x;  // float4 index: block gi / 8, lane j = gi % 8
-    const int64_t ib = gi >> 3;
-    const int j = threadIdx.x & 7;
-    const bool ok = ib < nblocks;
-    const float4 v = ok ? x[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+// One block's quantization by its 8 lanes (all 64 lanes of the wave take part in the DPP steps): lane j holds
+// elements 4j..4j+3 in v; returns qs dword j, and in lane 7 the d | s dword in hdr.
+template <int VARIANT> __device__ __forceinline__ uint32_t q8_1_lanes(const float4 v, int j, uint32_t& hdr) {
     float m = fmaxf(fmaxf(fmaxf(fmaxf(0.0f, fabsf(v.x)), fabsf(v.y)), fabsf(v.z)), fabsf(v.w));
     m = fmaxf(m, dpp_f<0xB1>(m));   // quad_perm [1,0,3,2]
     m = fmaxf(m, dpp_f<0x4E>(m));   // quad_perm [2,3,0,1]
@@ -251,10 +246,62 @@ __global__ __launch_bounds__(64) void quantize_q8_1_lanes_kernel(const float4* _
         }
         s = p;  // complete in lane 7
     }
+    hdr = f2h_bits(d) | (f2h_bits(s) << 16);
+    return qd;
+}
+
+template <int VARIANT>
+__global__ __launch_bounds__(64) void quantize_q8_1_lanes_kernel(const float4* __restrict__ x, uint32_t* __restrict__ y,
+                                                                 int64_t nblocks) {
+    const int64_t gi = (int64_t)blockIdx.x * 64 + threadIdx.x;  // float4 index: block gi / 8, lane j = gi % 8
+    const int64_t ib = gi >> 3;
+    const int j = threadIdx.x & 7;
+    const bool ok = ib < nblocks;
+    const float4 v = ok ? x[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t hdr;
+    const uint32_t qd = q8_1_lanes<VARIANT>(v, j, hdr);
     if (!ok) return;
     uint32_t* dst = y + ib * 9;
     dst[1 + j] = qd;
-    if (j == 7) dst[0] = f2h_bits(d) | (f2h_bits(s) << 16);
+    if (j == 7) dst[0] = hdr;
+}
+
+// Q8_1 straight into the tiled activation layout (LAY_TILED_ACT, qg_kernels.hpp): block b of token m lands in
+// token tile m / 16, stage b / 4, at (m % 16) * 144 + (b % 4) * 36 of that (tile, stage)'s 2304-B run; tokens
+// past M (to a multiple of 16) and blocks past K / 32 (to a multiple of 4) are zero blocks (d = s = 0, qs = 0:
+// an exact +0 term against any weights). Same bytes per real block as quantize_q8_1_lanes_kernel.
+__device__ __forceinline__ int64_t tiled_act_dword(int m, int b, int H) {
+    return ((((int64_t)(m / ACT_TILE) * H + b / 4) * ACT_TILE + m % ACT_TILE) * 4 + b % 4) * 9;
+}
+__global__ __launch_bounds__(64) void quantize_q8_1_tiled_kernel(const float4* __restrict__ x, uint32_t* __restrict__ y, int M,
+                                                                 int nb, int H, int64_t nblk) {
+    const int64_t gi = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    const int64_t ib = gi >> 3;  // padded block index, token-major over 4 H blocks per token
+    const int j = threadIdx.x & 7;
+    const bool ok = ib < nblk;
+    const int m = (int)(ib / (4 * H)), b = (int)(ib - (int64_t)m * 4 * H);
+    const bool real = ok && m < M && b < nb;
+    const float4 v = real ? x[((int64_t)m * nb + b) * 8 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t hdr;
+    const uint32_t qd = q8_1_lanes<0>(v, j, hdr);
+    if (!ok) return;
+    uint32_t* dst = y + tiled_act_dword(m, b, H);
+    dst[1 + j] = qd;
+    if (j == 7) dst[0] = real ? hdr : 0u;
+}
+
+// Q8_1 rows [M][K/32] -> the tiled activation layout (one thread per destination dword)
+__global__ __launch_bounds__(256) void tile_activations_kernel(const uint32_t* __restrict__ a, uint32_t* __restrict__ y, int M,
+                                                               int nb, int H, int64_t ndw) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= ndw) return;
+    const int64_t blk = i / 9;
+    const int w = (int)(i - blk * 9);
+    const int64_t st = blk / (ACT_TILE * 4);  // (tile, stage) run
+    const int r = (int)(blk - st * ACT_TILE * 4), t = r / 4, bl = r % 4;
+    const int tile = (int)(st / H), h = (int)(st - (int64_t)tile * H);
+    const int m = tile * ACT_TILE + t, b = h * 4 + bl;
+    y[i] = m < M && b < nb ? a[((int64_t)m * nb + b) * 9 + w] : 0u;
 }
 
 // FP16 -> Q8_1 with the fused kernel's semantics (kernels/gemm/gemm_fused.cuh:76-143), the
@@ -379,6 +426,27 @@ hipError_t launch_quantize(int type, int variant, const float* x, void* y, int64
         case FMT_Q5_1: return lq<FMT_Q5_1, 0>(x, y, nblocks, st);
     }
     return hipErrorInvalidValue;
+}
+
+size_t tiled_act_bytes(int M, int K) {
+    const int nb = K / QK, H = (nb + 3) / 4;
+    return (size_t)((M + ACT_TILE - 1) / ACT_TILE) * (size_t)H * ACT_STG;
+}
+
+hipError_t launch_quantize_q8_1_tiled(const float* x, void* y, int M, int K, hipStream_t st) {
+    const int nb = K / QK, H = (nb + 3) / 4;
+    const int64_t nblk = (int64_t)((M + ACT_TILE - 1) / ACT_TILE) * ACT_TILE * 4 * H;
+    hipLaunchKernelGGL(quantize_q8_1_tiled_kernel, dim3((unsigned)((nblk + 7) / 8)), dim3(64), 0, st, (const float4*)x,
+                       (uint32_t*)y, M, nb, H, nblk);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_activations(const void* a, void* y, int M, int K, hipStream_t st) {
+    const int nb = K / QK, H = (nb + 3) / 4;
+    const int64_t ndw = (int64_t)tiled_act_bytes(M, K) / 4;
+    hipLaunchKernelGGL(tile_activations_kernel, dim3((unsigned)((ndw + 255) / 256)), dim3(256), 0, st, (const uint32_t*)a,
+                       (uint32_t*)y, M, nb, H, ndw);
+    return hipGetLastError();
 }
 
 hipError_t launch_quantize_f16_fused(const void* x, void* y, int64_t nblocks, hipStream_t st) {

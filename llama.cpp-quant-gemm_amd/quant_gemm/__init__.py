@@ -272,6 +272,53 @@ def gemm_w4a8_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: i
     return out
 
 
+def quantize_q8_1_tiled(x: torch.Tensor) -> torch.Tensor:
+    """FP32 [M, K] -> the tiled activation layout (qg_quantize_q8_1_tiled): 1-D uint8 of
+    qg_activations_tiled_bytes(M, K) — 16-token tiles x 4-block stages, each a contiguous 2304-B run, zero
+    padded. Feed it to gemm_w4a8_tiled_act."""
+    _require(x.is_cuda and x.dtype == torch.float32 and x.dim() == 2, "x must be a 2-D CUDA float32 tensor")
+    M, K = x.shape
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    lib = _lib.load()
+    xc = x.contiguous()
+    out = torch.empty(lib.qg_activations_tiled_bytes(M, K), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        _lib.check(lib.qg_quantize_q8_1_tiled(_ptr(xc), _ptr(out), M, K, _stream(x.device)), "quantize_q8_1_tiled")
+    return out
+
+
+def tile_activations(activation_q: torch.Tensor, M: int, K: int) -> torch.Tensor:
+    """Q8_1 rows [M, K/32] -> the tiled activation layout (qg_tile_activations)."""
+    _require(activation_q.is_cuda and activation_q.dtype == torch.uint8, "activation_q must be a CUDA uint8 tensor")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    _require(activation_q.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    lib = _lib.load()
+    a = activation_q.contiguous()
+    out = torch.empty(lib.qg_activations_tiled_bytes(M, K), dtype=torch.uint8, device=a.device)
+    with torch.cuda.device(a.device):
+        _lib.check(lib.qg_tile_activations(_ptr(a), _ptr(out), M, K, _stream(a.device)), "tile_activations")
+    return out
+
+
+def gemm_w4a8_tiled_act(activation_tiled: torch.Tensor, weight_tiled: torch.Tensor, M: int, N: int, K: int,
+                        wtype: int = Q4_0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C [M, N] = gemm_w4a8_tiled's product with the activations in the tiled layout too
+    (qg_gemm_w4a8_tiled_act)."""
+    _require(activation_tiled.is_cuda and weight_tiled.is_cuda, "Inputs must be CUDA tensors")
+    _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
+    lib = _lib.load()
+    _require(activation_tiled.numel() == lib.qg_activations_tiled_bytes(M, K), "Tiled activation shape mismatch")
+    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=weight_tiled.device)
+    _require(out.is_cuda and out.dtype == torch.float32 and out.shape == (M, N) and out.is_contiguous(),
+             "out must be a contiguous CUDA float32 [M, N] tensor")
+    with torch.cuda.device(weight_tiled.device):
+        _lib.check(lib.qg_gemm_w4a8_tiled_act(_ptr(activation_tiled), _ptr(weight_tiled), _ptr(out), M, N, K, wtype,
+                                              _stream(weight_tiled.device)), "gemm_w4a8_tiled_act")
+    return out
+
+
 def quantize_q8_1_padded(x: torch.Tensor) -> torch.Tensor:
     """x float32 [M, K] -> uint8 [M, K'/32, 36] (qg_quantize_q8_1_padded): each row's blocks as
     quantize_q8_1, then zero blocks up to K'/32 = round_up(K/32, 8) — the activation side of the
@@ -474,6 +521,26 @@ def debug_sumi_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: 
     return out
 
 
+def debug_sumi_tiled_act(activation_tiled: torch.Tensor, weight_tiled: torch.Tensor, M: int, N: int, K: int,
+                         wtype: int = Q4_0) -> torch.Tensor:
+    """Per-block int32 dots [M, N, K/32] from the instantiation gemm_w4a8_tiled_act launches."""
+    lib = _lib.load()
+    _require(activation_tiled.numel() == lib.qg_activations_tiled_bytes(M, K), "Tiled activation shape mismatch")
+    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    out = torch.empty((M, N, K // 32), dtype=torch.int32, device=weight_tiled.device)
+    with torch.cuda.device(weight_tiled.device):
+        _lib.check(lib.qg_debug_sumi_tiled_act(_ptr(activation_tiled), _ptr(weight_tiled), _ptr(out), M, N, K, wtype,
+                                               _stream(weight_tiled.device)), "debug_sumi_tiled_act")
+    return out
+
+
+def debug_config_tiled_act(M: int, N: int, K: int, wtype: int = Q4_0, sumi: bool = False) -> str:
+    """The instantiation gemm_w4a8_tiled_act (or debug_sumi_tiled_act) launches; nothing runs."""
+    buf = ctypes.create_string_buffer(256)
+    _lib.check(_lib.load().qg_debug_config_tiled_act(M, N, K, wtype, int(sumi), buf, 256), "debug_config_tiled_act")
+    return buf.value.decode()
+
+
 def debug_config_tiled(M: int, N: int, K: int, wtype: int = Q4_0, sumi: bool = False) -> str:
     """The instantiation gemm_w4a8_tiled (or debug_sumi_tiled with sumi=True) launches; nothing runs."""
     buf = ctypes.create_string_buffer(256)
@@ -499,5 +566,6 @@ __all__ = [
     "gemm_w4a8_f32", "gemm_q4_0_fp16_fused", "quantize_q8_1_f16_fused", "gemm_w8a8", "gemm_q8_0_q8_1",
     "gemm_w4a16", "gemm_w8a16", "gemm_q4_0_fp32",
     "tile_weights", "gemm_w4a8_tiled", "debug_sumi_tiled", "debug_config_tiled",
+    "quantize_q8_1_tiled", "tile_activations", "gemm_w4a8_tiled_act", "debug_sumi_tiled_act", "debug_config_tiled_act",
     "Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q8_1",
 ]

@@ -43,6 +43,13 @@ SIGNATURES = {
     "qg_gemm_w4a8_tiled_ldc": ([P, P, P, I, I, I, I64, I, P], I),
     "qg_debug_sumi_tiled": ([P, P, P, I, I, I, I, P], I),
     "qg_debug_config_tiled": ([I, I, I, I, I, ctypes.c_char_p, SZ], I),
+    "qg_activations_tiled_bytes": ([I, I], SZ),
+    "qg_quantize_q8_1_tiled": ([P, P, I, I, P], I),
+    "qg_tile_activations": ([P, P, I, I, P], I),
+    "qg_gemm_w4a8_tiled_act": ([P, P, P, I, I, I, I, P], I),
+    "qg_gemm_w4a8_tiled_act_ldc": ([P, P, P, I, I, I, I64, I, P], I),
+    "qg_debug_sumi_tiled_act": ([P, P, P, I, I, I, I, P], I),
+    "qg_debug_config_tiled_act": ([I, I, I, I, I, ctypes.c_char_p, SZ], I),
     "qg_gemm_w4a8_padded": ([P, P, P, I, I, I, I, P], I),
     "qg_gemm_q4_0_q8_1": ([P, P, P, I, I, I, P], I),
     "qg_gemm_q4_1_q8_1": ([P, P, P, I, I, I, P], I),

@@ -308,6 +308,21 @@ def tile_weights(b_q: np.ndarray, t: int) -> np.ndarray:
     return np.ascontiguousarray(out).reshape(-1)
 
 
+def tile_activations(a_q: np.ndarray) -> np.ndarray:
+    """numpy restatement of the tiled activation layout (qg_quantize_q8_1_tiled / qg_tile_activations, round 5;
+    LAY_TILED_ACT in llama.cpp-quant-gemm_amd/csrc/qg_kernels.hpp): [M, K/32, 36] Q8_1 block bytes -> 1-D
+    bytes, tokens in tiles of 16, K/32 in stages of 4 blocks, each (token tile, stage) one 2304-B run
+    [token][block][36 B], zero blocks for tokens past M and blocks past K/32. A layout check for the tests;
+    not an oracle of the reference (the reference has no tiled layout)."""
+    m, nb, bb = a_q.shape
+    assert bb == 36
+    tiles, stages = -(-m // 16), -(-nb // 4)
+    full = np.zeros((tiles * 16, stages * 4, 36), np.uint8)
+    full[:m, :nb] = a_q
+    out = full.reshape(tiles, 16, stages, 4, 36).transpose(0, 2, 1, 3, 4)  # [tile][stage][token][block][byte]
+    return np.ascontiguousarray(out).reshape(-1)
+
+
 def _h(x: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(x).view(np.float16).astype(np.float32)[..., 0]
 

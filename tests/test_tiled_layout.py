@@ -64,3 +64,21 @@ def test_tile_weights_is_a_permutation_of_the_real_bytes(t):
     tiled = O.tile_weights(lo, t)
     assert np.count_nonzero(tiled) == n * nb * bb
     assert np.array_equal(np.sort(tiled[tiled != 0]), np.sort(lo.reshape(-1)))
+
+
+@pytest.mark.parametrize("m,nb", [(1, 1), (16, 4), (17, 129), (40, 8), (3, 5)])
+def test_tile_activations_placement(m, nb):
+    """oracle.tile_activations against the per-block placement formula the device kernels implement
+    (qg_quantize.hip tiled_act_dword): block b of token m at (((m / 16) * H + b / 4) * 16 + m % 16) * 144 +
+    (b % 4) * 36 with H = ceil(nb / 4) stages; everything else zero."""
+    rng = np.random.default_rng(m * 1000 + nb)
+    aq = rng.integers(0, 256, (m, nb, 36), dtype=np.uint8)
+    got = O.tile_activations(aq)
+    H, tiles = -(-nb // 4), -(-m // 16)
+    assert got.size == tiles * H * 2304
+    want = np.zeros(got.size, np.uint8)
+    for mm in range(m):
+        for b in range(nb):
+            o = (((mm // 16) * H + b // 4) * 16 + mm % 16) * 144 + (b % 4) * 36
+            want[o:o + 36] = aq[mm, b]
+    assert np.array_equal(got, want)
