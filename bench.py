@@ -226,7 +226,7 @@ def measure_config(wname: str, M: int, N: int, K: int, dev, G: int = 64, reps: i
             row["ref_published_gflops"], row["ref_source"] = pub
             row["vs_ref_published"] = round(tops * 1e3 / pub[0], 2)
         if M >= 128 and form != "w16":
-            cfg = f"{wname}_m{M}_n{N}_k{K}" + ("_tiled" if form == "tiled" else "")
+            cfg = f"{wname}_m{M}_n{N}_k{K}" + {"tiled": "_tiled", "tiled_act": "_tiled_act"}.get(form, "")
             row["mfma"] = {"frac_dense_i8_peak": round(tops / I8_DENSE_PEAK_TOPS, 4), "peak_tops": I8_DENSE_PEAK_TOPS,
                            "busy": load_pmc(cfg, "mfma_busy_frac"),
                            "note": "busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles) from a recorded --pmc pass "
