@@ -80,6 +80,25 @@ __device__ __forceinline__ uint32_t spread4_bit4(uint32_t x) {
     return ((uint32_t)__umul24(x, 0x00204081u) & 0x01010101u) << 4;
 }
 
+constexpr int TILE_ROWS = 32;  // weight rows per tile of LAY_TILED
+
+// One (tile, stage) of LAY_TILED: 32 rows x 4 blocks = 128 * BB bytes, as planes
+//   QS  [row tile i of 16 rows][half][lane = q * 16 + r][16 B]: dword q of the 4 blocks' qs of row
+//       16 i + r (half 1, Q8_0 only: dword 4 + q) — exactly MFMA lane (r, q)'s k-slot of each block;
+//   QH  [row][16 B]: the 4 blocks' qh dwords (Q5_0 / Q5_1);
+//   SC  [row][SCB]: f16 d of blocks 0..3, then (Q4_1 / Q5_1) f16 m of blocks 0..3.
+// Rows past N and blocks past K/32 are zero bytes (d = 0: an exact +0 term).
+template <int F> struct tiled_fmt {
+    using T = wfmt<F>;
+    static constexpr int QSL = T::Q8 ? 32 : 16;       // qs bytes per lane and row tile
+    static constexpr int QSB = 2 * 64 * QSL;          // QS plane bytes
+    static constexpr int QHB = T::QH >= 0 ? 16 : 0;   // qh bytes per row
+    static constexpr int SCB = T::MOFF >= 0 ? 16 : 8; // scale bytes per row
+    static constexpr int OQH = QSB, OSC = QSB + TILE_ROWS * QHB;
+    static constexpr int STG = OSC + TILE_ROWS * SCB;  // bytes per (tile, stage)
+    static_assert(STG == TILE_ROWS * 4 * T::BB, "the planes hold exactly the stage's blocks");
+};
+
 // Decoded weight block: q[i] = elements 4i..4i+3 (i<4) / 16+4(i-4).. (i>=4), i.e. elements 4i..4i+3,
 // exactly the stored values (no offset removed; unsigned nibbles, or Q8_0's signed bytes), plus its
 // scale(s).

@@ -74,24 +74,7 @@ constexpr int MMQ_BIAS = 0x4B400000;  // bits of 12582912.0f = 1.5 * 2^23
 constexpr float MMQ_BIAS_F = 12582912.0f;
 constexpr int MMQ_SB = 4;             // blocks per stage
 
-constexpr int TILE_ROWS = 32;  // weight rows per tile of LAY_TILED
-
-// One (tile, stage) of LAY_TILED: 32 rows x 4 blocks = 128 * BB bytes, as planes
-//   QS  [row tile i of 16 rows][half][lane = q * 16 + r][16 B]: dword q of the 4 blocks' qs of row
-//       16 i + r (half 1, Q8_0 only: dword 4 + q) — exactly MFMA lane (r, q)'s k-slot of each block;
-//   QH  [row][16 B]: the 4 blocks' qh dwords (Q5_0 / Q5_1);
-//   SC  [row][SCB]: f16 d of blocks 0..3, then (Q4_1 / Q5_1) f16 m of blocks 0..3.
-// Rows past N and blocks past K/32 are zero bytes (d = 0: an exact +0 term).
-template <int F> struct tiled_fmt {
-    using T = wfmt<F>;
-    static constexpr int QSL = T::Q8 ? 32 : 16;       // qs bytes per lane and row tile
-    static constexpr int QSB = 2 * 64 * QSL;          // QS plane bytes
-    static constexpr int QHB = T::QH >= 0 ? 16 : 0;   // qh bytes per row
-    static constexpr int SCB = T::MOFF >= 0 ? 16 : 8; // scale bytes per row
-    static constexpr int OQH = QSB, OSC = QSB + TILE_ROWS * QHB;
-    static constexpr int STG = OSC + TILE_ROWS * SCB;  // bytes per (tile, stage)
-    static_assert(STG == TILE_ROWS * MMQ_SB * T::BB, "the planes hold exactly the stage's blocks");
-};
+// TILE_ROWS, tiled_fmt: the tiled weight layout, qg_common.hpp (shared with the tiled GEMV)
 
 // 32 bits at byte offset (compile-time OFF) of an LDS row, from aligned dword reads.
 template <int OFF> __device__ __forceinline__ uint32_t lds32(const uint8_t* base) {
