@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--w16", action="store_true", help="FP32 activations through qg_gemm_w4a16_ws (Q4_0) / w8a16 (Q8_0)")
     ap.add_argument("--tiled", action="store_true", help="the tiled weight layout (qg_tile_weights + qg_gemm_w4a8_tiled)")
+    ap.add_argument("--tiled-act", action="store_true", help="tiled weights and tiled activations (qg_gemm_w4a8_tiled_act)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -33,6 +34,9 @@ def main() -> None:
     x = torch.rand((a.m, a.k), generator=g, device=dev) * 2 - 1
     w = torch.rand((a.n, a.k), generator=g, device=dev) * 2 - 1
     xq, wq = qg.quantize_q8_1(x), qg.quantize(w, a.wtype)
+    if a.tiled_act:
+        a.tiled = True
+        xt = qg.quantize_q8_1_tiled(x)
     if a.tiled:
         wq = qg.tile_weights(wq, a.n, a.k, a.wtype)
     R = max(2, math.ceil(600e6 / wq.numel()))
@@ -49,6 +53,9 @@ def main() -> None:
         if a.w16:
             rc = fn(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()), ctypes.c_void_p(out.data_ptr()),
                     a.m, a.n, a.k, ctypes.c_void_p(ws.data_ptr()), wsb, st)
+        elif a.tiled_act:
+            rc = lib.qg_gemm_w4a8_tiled_act(ctypes.c_void_p(xt.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
+                                            ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)
         elif a.tiled:
             rc = lib.qg_gemm_w4a8_tiled(ctypes.c_void_p(xq.data_ptr()), ctypes.c_void_p(copies[i % R].data_ptr()),
                                         ctypes.c_void_p(out.data_ptr()), a.m, a.n, a.k, a.wtype, st)
