@@ -98,7 +98,11 @@ size_t qg_gemm_w4a8_workspace_size(int M, int N, int K, int wtype);
 int qg_gemm_w4a8_ws(const void* A_q8_1, const void* B, float* C, int M, int N, int K, int wtype, void* workspace,
                     size_t workspace_bytes, qg_stream_t stream);
 
-/* Load-time weight layout for K/32 not a multiple of 8 (e.g. K = 4128): rows of K'/32 blocks,
+/* (Round 5: for weights reused across calls the tiled layout below — qg_tile_weights +
+ * qg_gemm_w4a8_tiled, or qg_gemm_w4a8_tiled_act with tiled activations — is the faster route for odd K/32
+ * as well: M = 32, K = 4128 6.1-6.2 us against 7.4 us here and 7.2 us for qg_gemm_w4a8_padded; DESIGN.md §6.
+ * The padded rows below stay for callers that keep the reference row layout.)
+ * Load-time weight layout for K/32 not a multiple of 8 (e.g. K = 4128): rows of K'/32 blocks,
  * K'/32 = round_up(K/32, 8), the real blocks first and then zero blocks (d = 0: every padded term is
  * an exact +0 of the reference's sum). qg_repack_weights writes B_packed (16-B aligned,
  * qg_repack_weights_bytes(N, K, wtype) bytes) from B [N][K/32]; one streaming kernel.
