@@ -199,8 +199,12 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__
 //   amax: max over the 8 lanes' partial maxima (v_max_f32 is order-free on non-NaN values; every partial
 //     starts at 0.0f as the sequential loop does, so NaN inputs are ignored the same way);
 //   s = sum(x) in ELEMENT order: the partial sum walks the 8 lanes in turn (lane j adds its 4 elements to
-//     what lane j - 1 handed over by DPP row_shr:1), the very sequence of fp32 adds of the reference loop;
-//   variant 1: s = d * sum(q) (an integer sum, any order).
+//     what lane j - 1 handed over by DPP row_shr:1), the very sequence of fp32 adds of the reference loop.
+//     Every lane runs every step (no select): after step t lane j holds the ordered sum of lanes j - t..j,
+//     and lane 7's step-7 value reaches back only to lane 0's step-0 value 0 + x, so what a group's first
+//     lane receives from the previous group (or a row edge) never enters lane 7's result;
+//   variant 1: s = d * sum(q) (an integer sum, any order);
+//   roundf and d = m / 127 through roundf_rc / div127 (qg_quant_block.hpp: same results, fewer instructions).
 // Lane j stores qs dword j; lane 7 (which ends holding s) stores the d | s dword.
 // One block's quantization by its 8 lanes (all 64 lanes of the wave take part in the DPP steps): lane j holds
 // elements 4j..4j+3 in v; returns qs dword j, and in lane 7 the d | s dword in hdr.
@@ -221,15 +225,18 @@ template <int VARIANT> __device__ __forceinline__ uint32_t q8_1_lanes(const floa
             qd |= ((uint32_t)(int)r & 0xFFu) << (8 * e);
         }
     } else {
-        d = m / 127.0f;
+        d = div127(m);
         const float id = d > 0.0f ? 1.0f / d : 0.0f;
+        uint32_t t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            int t = (int)roundf(xs[e] * id);
-            t = VARIANT == 1 ? max(-127, min(127, t)) : max(-128, min(127, t));
-            sq += t;
-            qd |= ((uint32_t)t & 0xFFu) << (8 * e);
+            const int q = roundf_rc(xs[e] * id);  // |q| <= 127 unless d is subnormal (inexact): clamp kept
+            const int c = VARIANT == 1 ? max(-127, min(127, q)) : max(-128, min(127, q));
+            sq += c;
+            t[e] = (uint32_t)c;
         }
+        // low bytes of t[0..3] into one dword: two byte permutes and an or
+        qd = __builtin_amdgcn_perm(t[1], t[0], 0x0c0c0400u) | __builtin_amdgcn_perm(t[3], t[2], 0x04000c0cu);
     }
     float s;
     if constexpr (VARIANT == 1) {
@@ -238,32 +245,32 @@ template <int VARIANT> __device__ __forceinline__ uint32_t q8_1_lanes(const floa
         sq += __builtin_amdgcn_update_dpp(0, sq, 0x141, 0xF, 0xF, false);
         s = (float)sq * d;
     } else {
-        float p = 0.0f;
+        float p = (((0.0f + v.x) + v.y) + v.z) + v.w;
 #pragma unroll
-        for (int step = 0; step < 8; ++step) {
-            if (j == step) p = (((p + v.x) + v.y) + v.z) + v.w;
-            if (step < 7) p = dpp_f<0x111>(p);  // row_shr:1: lane step + 1 takes the running sum
-        }
+        for (int step = 1; step < 8; ++step) p = (((dpp_f<0x111>(p) + v.x) + v.y) + v.z) + v.w;  // row_shr:1
         s = p;  // complete in lane 7
     }
     hdr = f2h_bits(d) | (f2h_bits(s) << 16);
     return qd;
 }
 
-template <int VARIANT>
+// I: the index type — uint32_t where every float4 index and output dword fits (the launcher's choice; fewer
+// address instructions on the one-wave-per-workgroup critical path), int64_t otherwise.
+// FULL: the grid covers exactly nblocks (nblocks % 8 == 0): no bounds predicate.
+template <int VARIANT, typename I, bool FULL>
 __global__ __launch_bounds__(64) void quantize_q8_1_lanes_kernel(const float4* __restrict__ x, uint32_t* __restrict__ y,
-                                                                 int64_t nblocks) {
-    const int64_t gi = (int64_t)blockIdx.x * 64 + threadIdx.x;  // float4 index: block gi / 8, lane j = gi % 8
-    const int64_t ib = gi >> 3;
+                                                                 I nblocks) {
+    const I gi = (I)blockIdx.x * 64 + threadIdx.x;  // float4 index: block gi / 8, lane j = gi % 8
+    const I ib = gi >> 3;
     const int j = threadIdx.x & 7;
-    const bool ok = ib < nblocks;
+    const bool ok = FULL || ib < nblocks;
     const float4 v = ok ? x[gi] : make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t hdr;
     const uint32_t qd = q8_1_lanes<VARIANT>(v, j, hdr);
     if (!ok) return;
-    uint32_t* dst = y + ib * 9;
-    dst[1 + j] = qd;
-    if (j == 7) dst[0] = hdr;
+    uint32_t* dst = y + (gi + ib);  // = block ib's dword j (9 ib + j): qs dword j at +1, the header at -j
+    dst[1] = qd;
+    if (j == 7) dst[-7] = hdr;
 }
 
 // Q8_1 straight into the tiled activation layout (LAY_TILED_ACT, qg_kernels.hpp): block b of token m lands in
@@ -394,8 +401,16 @@ template <int TYPE, int VARIANT>
 hipError_t lq(const float* x, void* y, int64_t nblocks, hipStream_t st) {
     if constexpr (TYPE == FMT_Q8_1) {
         if (((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 3) == 0 && (nblocks + 7) / 8 <= 0x7fffffffL) {
-            hipLaunchKernelGGL((quantize_q8_1_lanes_kernel<VARIANT>), dim3((unsigned)((nblocks + 7) / 8)), dim3(64), 0, st,
-                               (const float4*)x, (uint32_t*)y, nblocks);
+            const dim3 grid((unsigned)((nblocks + 7) / 8));
+            if (nblocks <= (int64_t(1) << 26) && nblocks % 8 == 0)
+                hipLaunchKernelGGL((quantize_q8_1_lanes_kernel<VARIANT, uint32_t, true>), grid, dim3(64), 0, st,
+                                   (const float4*)x, (uint32_t*)y, (uint32_t)nblocks);
+            else if (nblocks <= (int64_t(1) << 26))
+                hipLaunchKernelGGL((quantize_q8_1_lanes_kernel<VARIANT, uint32_t, false>), grid, dim3(64), 0, st,
+                                   (const float4*)x, (uint32_t*)y, (uint32_t)nblocks);
+            else
+                hipLaunchKernelGGL((quantize_q8_1_lanes_kernel<VARIANT, int64_t, false>), grid, dim3(64), 0, st,
+                                   (const float4*)x, (uint32_t*)y, nblocks);
             return hipGetLastError();
         }
     }
