@@ -184,7 +184,10 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // PRE: read the unit's LDS records into registers right after the staging barrier, before the
 // first weight byte is used, so the LDS latency overlaps the weight stream and only VALU work
 // remains once the weights land (MT <= 2: 12 * BPL * MT dwords of registers).
-// ONEU: every lane owns at most one unit (K <= 32 * BPL * LPR): the kernel has no unit loop, so the
+// ONEU > 1 (round 5): every lane owns at most ONEU units (K <= 32 * BPL * LPR * ONEU), all their weight loads
+// issued before the activation staging, no unit loop: ONEU units of weights in flight per lane instead of the
+// loop's two (the published K = 14336 decode shapes, VERDICT r04 missing #1).
+// ONEU == 1: every lane owns at most one unit (K <= 32 * BPL * LPR): the kernel has no unit loop, so the
 // waits for the weight loads sit at their first use, behind the record reads (with a loop in the
 // kernel, hipcc's wait insertion falls back to vmcnt(0) before the first record read).
 // Argument order: everything the first loads need (A, B, their batch strides, M, N, K) sits in the
@@ -200,11 +203,12 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, bool ONEU, int TPW = 1>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, int ONEU, int TPW = 1>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
                                           int32_t* __restrict__ sumi_out, int tile_in = -1) {
-    static_assert(TPW == 1 || ONEU, "several tiles per workgroup: loop-free form only");
+    static_assert(TPW == 1 || ONEU == 1, "several tiles per workgroup: the one-unit form only");
+    constexpr int NUN = ONEU > 1 ? ONEU : 1;  // weight units in registers per lane (loop-free forms)
     using G = gemv_geom<F, BPL>;
     A = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(A) + blockIdx.y * sA);
     B += blockIdx.y * sB;
@@ -256,10 +260,13 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     };
     // record of activation block blk = m * nb + b: unit (m * U + b / BPL) = blk / BPL, slot b % BPL
     auto rec_of = [&](int blk) { return (blk / BPL) * G::REC_DW + (blk % BPL) * 12; };
-    uint32_t cur[G::UDW];
+    uint32_t curs[NUN][G::UDW];
+    uint32_t(&cur)[G::UDW] = curs[0];
     uint32_t more[TPW > 1 ? TPW - 1 : 1][G::UDW];  // tiles 1.. of the workgroup (TPW > 1)
     auto load_first = [&]() {
         load_unit(cur, lir);
+#pragma unroll
+        for (int j = 1; j < NUN; ++j) load_unit(curs[j], lir + j * LPR);
 #pragma unroll
         for (int t = 1; t < TPW; ++t) load_unit(more[t - 1], lir, t);
     };
@@ -348,8 +355,17 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
         // tiles 1.. after tile 0 (below): the records read once, each tile its own sum and store
         static_assert(!SUMI || TPW == 1, "parity hook: one tile per workgroup");
     }
-    if constexpr (ONEU) {
+    if constexpr (ONEU == 1) {
         if (lir < U) do_unit(lir);
+    } else if constexpr (ONEU > 1) {
+#pragma unroll
+        for (int j = 0; j < NUN; ++j) {
+            const int u = lir + j * LPR;
+            if (u < U) {
+                read_pre(u);
+                dot_unit(curs[j], u, row, row_ok);
+            }
+        }
     } else {
         for (int j = 0; j < iters; ++j) {
             const int u = lir + j * LPR;
@@ -389,7 +405,7 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
 }
 
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool NT = false, bool PRE = (MT <= 2),
-          bool ONEU = false, int TPW = 1>
+          int ONEU = 0, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                    long sA, long sB, int M, int N, int K, float* __restrict__ C,
                                                    long sC, long ldc_m, long ldc_n, int32_t* __restrict__ sumi_out) {
@@ -398,7 +414,7 @@ __global__ __launch_bounds__(WGS) void gemv_kernel(const uint32_t* __restrict__ 
 
 // M = 2..8, one product: (A, B, M, N, K, out, ldc_m, ldc_n) with 32-bit output strides = 10 dwords
 // (the general entry preloads 14 and s_loads the rest).
-template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool PRE = (MT <= 2), bool ONEU = false>
+template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool PRE = (MT <= 2), int ONEU = 0>
 __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int M,
                                                     int N, int K, void* __restrict__ out, int ldc_m, int ldc_n) {
     gemv_body<F, MT, BPL, LPR, WGS, SUMI, AIN, false, PRE, ONEU>(A, B, 0, 0, M, N, K, SUMI ? nullptr : (float*)out, 0,
@@ -410,7 +426,7 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
 // entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
-template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, bool ONEU = false>
+template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, int ONEU = 0>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
                                                     int K, void* __restrict__ out) {
     gemv_body<F, 1, BPL, LPR, WGS, SUMI, AIN, false, true, ONEU>(A, B, 0, 0, 1, N, K, SUMI ? nullptr : (float*)out, 0, 0,
@@ -455,7 +471,7 @@ __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__
 #ifndef QG_GEMVG_WDIV
 #define QG_GEMVG_WDIV 2  // grouped launch workgroup size = the single launch's / QG_GEMVG_WDIV (below)
 #endif
-template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, bool ONEU, int TPW = 1>
+template <int F, int MT, int BPL, int LPR, int WGS, bool PRE, int ONEU, int TPW = 1>
 __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
     constexpr int RPB = (WGS / 64) * (64 / LPR) * TPW;  // rows per workgroup
     const int item = blockIdx.y;
@@ -468,6 +484,11 @@ __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
         reinterpret_cast<const uint32_t*>(d.A), reinterpret_cast<const uint8_t*>(d.B), 0, 0, grp.M, d.N, grp.K,
         d.C, 0, d.ldc, 1, nullptr, tile);
 }
+
+// Loop-free multi-unit single launches (ONEU = 2 / 4, above): 1 = on, 0 = the unit loop (A/B builds).
+#ifndef QG_GEMV_NU
+#define QG_GEMV_NU 1
+#endif
 
 // Host side -------------------------------------------------------------------------------------
 
@@ -495,12 +516,19 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const size_t lds = gemv_lds_bytes<F, BPL>(g.M, g.K);
     const int grid = (g.N + RPB - 1) / RPB;
     const bool one = g.K / QK / BPL <= LPR;
+    // units per lane of the loop-free multi-unit form: Q4_0 M = 1 single launches only (0: the unit loop).
+    // profiles/r05_tuning/r5zd_ab.txt, unit loop -> multi-unit: Q4_0 M = 1 K = 14336 7.69 -> 7.46 us, K = 11008
+    // 6.32 -> 6.17, K = 8192 5.02 -> 4.78; slower for M = 2..4 (8.93 -> 9.45 at M = 2), Q4_1 (8.02 -> 9.50) and
+    // Q8_0 (12.37 -> 12.53), which keep the loop
+    constexpr bool NU_OK = QG_GEMV_NU && MT == 1 && F == FMT_Q4_0;
+    const int nu_all = (g.K / QK / BPL + LPR - 1) / LPR;
+    const int nu = one ? 1 : !NU_OK ? 0 : nu_all <= 2 ? 2 : nu_all <= 4 ? 4 : 0;
     // M = 1, one product, unit output stride: the minimal-argument entry (gemv1_kernel)
     const bool m1 = MT == 1 && PRE && !NT && g.M == 1 && g.batch == 1 && g.ldc_n == 1;
     if (g.group && (SUMI || AIN != AIN_Q8_1 || NT || MT > 4)) return hipErrorInvalidValue;  // no grouped form here
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
         describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
-                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (int)one,
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), m1 ? nu : (int)one,
                         m1 ? "m1" : (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) ? "short" : "full", grid,
                         g.batch);
         return hipSuccess;
@@ -550,7 +578,11 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
         }
     }
     if (m1) {
-        auto k1 = one ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, true> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, false>;
+        auto k1 = nu == 1 ? gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, 1> : gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, 0>;
+        if constexpr (NU_OK) {
+            if (nu == 2) k1 = gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, 2>;
+            if (nu == 4) k1 = gemv1_kernel<F, BPL, LPR, WGS, SUMI, AIN, 4>;
+        }
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
@@ -561,8 +593,8 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     }
     // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)
     if (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) {
-        auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, true>
-                      : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), false>;
+        auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, 1>
+                      : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 0>;
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;

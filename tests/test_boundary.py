@@ -183,6 +183,12 @@ def test_headline_configs_kernels(lib):
     import quant_gemm as qg
     assert qg.debug_config(1, 4096, 4096, 2).startswith("gemv F=2 MT=1 BPL=2 LPR=64 WGS=1024")
     assert "ONEU=1" in qg.debug_config(1, 4096, 4096, 2)
+    # the published 4096 x 1 x 14336 decode shape: Q4_0 M = 1 loop-free with 4 units per lane (round 5);
+    # M = 2 and the other formats keep the unit loop (ONEU=0)
+    assert "MT=1 " in qg.debug_config(1, 4096, 14336, 2) and "ONEU=4 SIG=m1" in qg.debug_config(1, 4096, 14336, 2)
+    assert "ONEU=2 SIG=m1" in qg.debug_config(1, 4096, 8192, 2)
+    assert "ONEU=0" in qg.debug_config(2, 4096, 14336, 2) and "ONEU=0" in qg.debug_config(1, 4096, 14336, 3)
+    assert qg.debug_config(1, 4096, 14336, 2) == qg.debug_config(1, 4096, 14336, 2, sumi=True)
     assert qg.debug_config(32, 4096, 4096, 2).startswith("mmq F=2 ")
     assert "BN=32 TT=1 W=12 P16=1 NB=1 LAY=0 AW=0" in qg.debug_config(32, 4096, 4096, 2)
     # the tiled layout of the same config: same tile, same waves
