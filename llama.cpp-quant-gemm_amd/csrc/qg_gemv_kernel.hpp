@@ -489,6 +489,9 @@ __global__ __launch_bounds__(WGS) void gemvg_kernel(const GemvGroup grp) {
 #ifndef QG_GEMV_NU
 #define QG_GEMV_NU 1
 #endif
+#ifndef QG_GEMV_NU_MT
+#define QG_GEMV_NU_MT 1  // (A/B builds) the largest M tile that takes the multi-unit form
+#endif
 
 // Host side -------------------------------------------------------------------------------------
 
@@ -520,7 +523,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     // profiles/r05_tuning/r5zd_ab.txt, unit loop -> multi-unit: Q4_0 M = 1 K = 14336 7.69 -> 7.46 us, K = 11008
     // 6.32 -> 6.17, K = 8192 5.02 -> 4.78; slower for M = 2..4 (8.93 -> 9.45 at M = 2), Q4_1 (8.02 -> 9.50) and
     // Q8_0 (12.37 -> 12.53), which keep the loop
-    constexpr bool NU_OK = QG_GEMV_NU && MT == 1 && F == FMT_Q4_0;
+    constexpr bool NU_OK = QG_GEMV_NU && MT <= QG_GEMV_NU_MT && F == FMT_Q4_0;
     const int nu_all = (g.K / QK / BPL + LPR - 1) / LPR;
     const int nu = one ? 1 : !NU_OK ? 0 : nu_all <= 2 ? 2 : nu_all <= 4 ? 4 : 0;
     // M = 1, one product, unit output stride: the minimal-argument entry (gemv1_kernel)
@@ -528,7 +531,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     if (g.group && (SUMI || AIN != AIN_Q8_1 || NT || MT > 4)) return hipErrorInvalidValue;  // no grouped form here
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
         describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
-                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), m1 ? nu : (int)one,
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (m1 || (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX)) ? nu : (int)one,
                         m1 ? "m1" : (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) ? "short" : "full", grid,
                         g.batch);
         return hipSuccess;
@@ -595,6 +598,10 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     if (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) {
         auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, 1>
                       : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 0>;
+        if constexpr (NU_OK && MT > 1) {
+            if (nu == 2) ks = gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 2>;
+            if (nu == 4) ks = gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 4>;
+        }
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
