@@ -83,6 +83,24 @@ def test_quantizer_bytes_bit_exact(O, qg, t, variant):
         assert np.array_equal(got, want)
 
 
+def test_q8_1_quantizer_extreme_scales(O, qg):
+    """Q8_1 blocks whose d = amax / 127 is subnormal (amax in 5e-37 .. 1.5e-36: d keeps 21-23 significant bits)
+    or whose amax is near the float maximum, both quantizer variants:
+    bytes identical to the oracle (the lanes quantizer's fma-corrected division and 3-instruction roundf,
+    csrc/qg_quant_block.hpp, against the reference's IEEE division and roundf). Blocks whose 1 / d overflows
+    (amax below ~3.7e-37) are left out: there the reference converts inf / NaN to int, which C leaves undefined."""
+    rng = np.random.default_rng(11)
+    rows = [rng.uniform(-1.0, 1.0, 256).astype(np.float32) * np.float32(s) for s in (5e-37, 8e-37, 1.4e-36)]
+    rows.append(rng.uniform(-1.0, 1.0, 256).astype(np.float32) * np.float32(3.0e38))
+    x = np.stack(rows)
+    amax = np.abs(x.reshape(-1, 32)).max(axis=1)
+    assert ((amax > 3.7e-37) | (amax == 0)).all()
+    for variant in (0, 1):
+        got = host(qg.quantize(dev(x), 9, variant))
+        want = O.quantize(x, 9, variant)
+        assert np.array_equal(got, want), variant
+
+
 def test_quantize_reference_names(O, qg):
     a, b = O.fill_uniform_step4(3, 5, 1024)
     assert np.array_equal(host(qg.quantize_q8_1(dev(a))), O.quantize(a, O.Q8_1))
