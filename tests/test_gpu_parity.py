@@ -176,6 +176,22 @@ def test_gemv_long_rows(O, qg, t, m, n, k):
     assert_close_to_oracle(O, c2, aq2, bq2, t)
 
 
+@pytest.mark.parametrize("n,k,nu", [(70, 8192, 2), (33, 11008, 4), (4096, 14336, 4), (17, 12288, 4)])
+def test_gemv_multi_unit_sumi_and_output(O, qg, n, k, nu):
+    """The loop-free multi-unit GEMV (Q4_0, M = 1, K > 4096: every unit of a lane loaded before the staging,
+    qg_gemv_kernel.hpp ONEU = 2 / 4; round 5): the parity hook runs that exact instantiation and its int32
+    block dots equal the reference's inner loop (include/gemm_reference.h:202-212) bit for bit, incl. lanes
+    whose last unit is past the row (K = 11008: 172 units over 64 lanes) and the published 4096 x 1 x 14336."""
+    t, m = 2, 1
+    cfg = qg.debug_config(m, n, k, t)
+    assert f"ONEU={nu} SIG=m1" in cfg and cfg == qg.debug_config(m, n, k, t, sumi=True), cfg
+    _, _, aq, bq = make_case(O, m, n, k, t, seed=k)
+    _, want = O.gemm_w4a8(aq, bq, t, want_sumi=True)
+    assert np.array_equal(host(qg.debug_sumi(dev(aq), dev(bq), m, n, k, t)), want)
+    c = host(qg.gemm_w4a8(dev(aq), dev(bq), m, n, k, t))
+    assert_close_to_oracle(O, c, aq, bq, t)
+
+
 # ------------------------------------------------------------------------------- outputs
 @pytest.mark.parametrize("t", WTYPES)
 @pytest.mark.parametrize("m", [1, 2, 3, 4, 5, 8])
