@@ -612,6 +612,28 @@ def strong_legs(world: int, rank: int, dev, G: int, steps: int, warmup: int, M: 
                         "ranks), like for like per leg; DESIGN.md §7"}}
 
 
+def compact_summary(out: dict) -> dict:
+    """The bench line's figures in ~1.5 KB (the line's last key; see main)."""
+    r = out.get("roofline") or {}
+    sm = {"us": r.get("us_per_launch"), "frac": r.get("frac"), "floor_us": r.get("floor_us"),
+          "units_read_store_us": (r.get("floor") or {}).get("units_read_store_us")}
+    for k in ("batched", "grouped"):
+        if out.get(k):
+            sm[k + "_us"] = out[k]["us_per_gemv"]
+            sm[k + "_frac"] = out[k]["frac"]
+    if out.get("cpu_baseline"):
+        sm["cpu_1core_ms"] = out["cpu_baseline"].get("ms_per_gemv")
+    for x in out.get("cpu_baseline_mt") or []:
+        sm[f"cpu_{x.get('cores')}t_ms"] = x.get("ms_per_gemv")
+    if out.get("strong"):
+        sm["strong"] = {k: v for k, v in out["strong"].items() if "speedup" in k}
+    rows = []
+    for c in out.get("side_configs") or []:
+        rows.append(f"{c['wtype']}/{c['M']}x{c['N']}x{c['K']}/{c['form']}={c['us_per_launch']}@{c.get('frac_hbm')}")
+    sm["side"] = rows
+    return sm
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -947,6 +969,8 @@ def main() -> None:
             torch.cuda.empty_cache()
             sides = [("q4_0", 32, 4096, 4096, ("single", "tiled", "tiled_act"), "configs[2]"),
                      ("q4_0", 1, 4096, 4096, ("tiled",), "configs[1] on the tiled layout (decode GEMV)"),
+                     ("q4_0", 2, 4096, 4096, ("single", "tiled"), "decode M=2, both layouts"),
+                     ("q4_0", 4, 4096, 4096, ("single", "tiled"), "decode M=4, both layouts"),
                      ("q4_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q5_0", 1, 4096, 4096, ("single",), "configs[3]"), ("q5_1", 1, 4096, 4096, ("single",), "configs[3]"),
                      ("q4_0", 1, 32000, 4096, ("single", "batched"), "configs[4] on one GPU"),
@@ -959,10 +983,10 @@ def main() -> None:
                      # (docs/2d_tiling_final_report.md:70-74, weight-major 4096/8192 x tokens x 14336), the
                      # llama-shape batch-decode sweep (tests/test_llama_shapes.cu:6,256: 1..8 tokens at
                      # 4096 x 14336) and the step4 prefill sizes (tests/step4_w4a8_gemm.cu:278-281)
-                     ("q4_0", 1, 4096, 14336, ("single",), "published 4096x1x14336"),
-                     ("q4_0", 2, 4096, 14336, ("single",), "published 4096x2x14336"),
-                     ("q4_0", 3, 4096, 14336, ("single",), "llama-shape sweep"),
-                     ("q4_0", 4, 4096, 14336, ("single",), "published 4096x4x14336"),
+                     ("q4_0", 1, 4096, 14336, ("single", "tiled"), "published 4096x1x14336"),
+                     ("q4_0", 2, 4096, 14336, ("single", "tiled"), "published 4096x2x14336"),
+                     ("q4_0", 3, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
+                     ("q4_0", 4, 4096, 14336, ("single", "tiled"), "published 4096x4x14336"),
                      ("q4_0", 5, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
                      ("q4_0", 8, 4096, 14336, ("single", "tiled"), "llama-shape sweep"),
                      ("q4_0", 2, 8192, 14336, ("single",), "published 8192x2x14336"),
@@ -971,6 +995,10 @@ def main() -> None:
                      ("q4_0", 512, 4096, 14336, ("single", "tiled"), "step4 prefill")]
             out["side_configs"] = [r for (w, m_, n_, k_, f, lab) in sides
                                    for r in measure_config(w, m_, n_, k_, dev, forms=f, label=lab)]
+        # LAST key: the driver keeps only the tail of stdout, so a compact restatement of
+        # the figures above ends the line — headline, floor, batched / grouped, CPU rows and every side config
+        # as "wtype/MxNxK/form=us@frac_hbm"
+        out["summary"] = compact_summary(out)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

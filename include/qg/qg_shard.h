@@ -52,10 +52,15 @@ size_t qg_sharded_gemm_workspace_size(int M, int N, int world);
  * Returns QG_ERR_INVALID_ARG for a null comm / pointer, QG_ERR_BAD_K, QG_ERR_UNSUPPORTED without a
  * large enough workspace, QG_ERR_HIP for a launch or RCCL error (qg_shard_last_nccl_error).
  * Collective safety: errors in the arguments all ranks share (comm, M, N, K, A, C) are returned before
- * anything is enqueued, on every rank alike. An error local to one rank (a null B_shard with rows to
- * compute, a missing or small workspace, its kernel's launch) does NOT skip the collective: that rank
- * still enters the ncclAllGather with its slice set to NaN and returns the error afterwards, so its
- * peers finish the call (their C holds NaN in the failing rank's columns) instead of waiting forever. */
+ * anything is enqueued, on every rank alike; so is a missing / short workspace when N % world != 0 (its
+ * size is a function of (M, N, world) alone: pass it alike on every rank). An error local to one rank (a
+ * null B_shard with rows to compute, a missing or small workspace when N % world == 0, its kernel's
+ * launch) does NOT skip the collective, and its error path allocates nothing: that rank enters the
+ * ncclAllGather with its slice set to quiet NaN (0x7FC00000; without a workspace it receives into C),
+ * sets its own C to NaN and returns the error afterwards, so its peers finish the call instead of
+ * waiting forever. The peers return QG_OK with NaN in the failing rank's columns
+ * [rank * P, rank * P + rows): a caller that must know detects it with isnan on those columns or, as
+ * usual for rank-local errors, by exchanging the return codes (tests/test_sharded.py shows both). */
 int qg_sharded_gemm_w4a8(const void* A_q8_1, const void* B_shard, float* C, int M, int N, int K, int wtype,
                          void* workspace, size_t workspace_bytes, qg_nccl_comm_t comm, qg_stream_t stream);
 

@@ -140,7 +140,7 @@ bool is_weight_type(int t) {
     return t == QG_TYPE_Q4_0 || t == QG_TYPE_Q4_1 || t == QG_TYPE_Q5_0 || t == QG_TYPE_Q5_1 || t == QG_TYPE_Q8_0;
 }
 
-// Crossover from tools/archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
+// Crossover from profiles/tools_archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe_smallm.txt): the dot4 GEMV
 // wins up to M = 4 (its LDS activation reads grow with M), the MFMA kernel from M = 5 on.
 int select_algo(const GemmArgs& g) {
     if (g.M <= 4 && gemv_eligible(g)) return QG_ALGO_GEMV;
@@ -225,8 +225,11 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     return QG_OK;
 }
 
-// The tiled weight layout (qg_tile_weights): the tiled decode GEMV for M = 1 (qg_gemvt.hip), the MFMA
-// kernel beyond (LAY_TILED; odd K/32 through its activation windows).
+// The tiled weight layout (qg_tile_weights): the tiled decode GEMV for M <= 4 (qg_gemvt.hip, round 6), the
+// MFMA kernels beyond (LAY_TILED; odd K/32 through its activation windows). Shapes neither
+// takes (ldc past INT32_MAX, activation windows of 2 GiB or more, K/32 whose records exceed the LDS at
+// M <= 4 where the MFMA kernel rejects the shape too) return QG_ERR_UNSUPPORTED: the tiled layout has no
+// generic kernel.
 int run_tiled(GemmArgs& g, hipStream_t st) {
     if (g.M < 0 || g.N < 0) return QG_ERR_INVALID_ARG;
     if (g.K <= 0 || g.K % 32 != 0) return QG_ERR_BAD_K;
@@ -234,7 +237,7 @@ int run_tiled(GemmArgs& g, hipStream_t st) {
     if (g.M == 0 || g.N == 0) return QG_OK;
     if (!g.A || !g.B || (!g.C && !g.sumi)) return QG_ERR_INVALID_ARG;
     if (((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 15) != 0) return QG_ERR_ALIGN;
-    if (gemvt_eligible(g)) return hip_status(launch_gemvt(g, st));  // M = 1: the tiled decode GEMV
+    if (gemvt_eligible(g)) return hip_status(launch_gemvt(g, st));  // M <= 4: the tiled decode GEMV
     if (!mfma_eligible(g)) return QG_ERR_UNSUPPORTED;
     return hip_status(launch_mfma(g, st));
 }

@@ -1,6 +1,6 @@
 // qg_gemv.hip — product instantiations and dispatch of the GEMV kernels (qg_gemv_kernel.hpp).
 //
-// Configuration from the tuning sweeps (tools/archive/gemv_probe.hip, profiles/r01_tuning/): M <= 4 with
+// Configuration from the tuning sweeps (profiles/tools_archive/gemv_probe.hip, profiles/r01_tuning/): M <= 4 with
 // K >= 4096: 2-block units, 64 lanes (one wave) per row, 1024-thread workgroups (512 for M = 1 and
 // N >= 16384); otherwise 4-block units (72 B for Q4_0), 32 lanes per row, 512-thread workgroups;
 // short rows (K/32/4 < 32) 4 lanes per row; K/32 not a multiple of 4: 2-block units.

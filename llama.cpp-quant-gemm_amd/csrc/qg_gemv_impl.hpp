@@ -48,7 +48,7 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
         if (nb % 2 == 0 && nb / 2 >= 64) {
             if (MT == 1 && AIN == AIN_Q8_1 && g.N >= 16384 && g.K < 8192)
                 return gemv_launch<F, 1, 2, 64, QG_GEMVBIG_WGS, SUMI, AIN>(g, st);
-            // activation records preloaded into registers for M <= 4 (tools/archive/gemv_pre_probe.hip,
+            // activation records preloaded into registers for M <= 4 (profiles/tools_archive/gemv_pre_probe.hip,
             // profiles/r01_tuning/gemv_pre_probe.txt: M=3 4.76 -> 4.52 us, M=4 5.16 -> 5.04 us)
             // Q5_0 / Q5_1: 512-thread workgroups (profiles/r03_tuning/r03_ab_wgs.txt: M=1 3.82 -> 3.78 /
             // 3.93 -> 3.88 us; Q4_0 / Q8_0 are faster at 1024, Q4_1 equal)

@@ -1,6 +1,6 @@
 // qg_gemv_kernel.hpp — the W4A8 GEMV / small-batch kernels (M <= 8 activation rows).
 //
-// Included by qg_gemv.hip (the product's instantiations + dispatch) and by tools/archive/gemv_probe.hip
+// Included by qg_gemv.hip (the product's instantiations + dispatch) and by profiles/tools_archive/gemv_probe.hip
 // (the tuning sweep). Computes, for the reference's activation-major contract
 // C[M,N] = A_q8_1[M,K] . B_w[N,K]^T (include/gemm_reference.h:175-222):
 //   C[m*ldc_m + n*ldc_n] = sum_b term(A[m][b], B[n][b]).
@@ -154,6 +154,91 @@ template <int F, int BI> __device__ __forceinline__ float block_term_rec(const u
 }
 
 // ------------------------------------------------------------------------------------------------
+// Weight units on the tiled layout (LAY_TILED / LAY_TILED_ACT; tiled_fmt in qg_common.hpp), round 6: the
+// decode GEMV of qg_gemvt.hip. A lane's unit is BPL = 4 blocks (one stage) of ONE weight row — the same bytes
+// as a 4-block unit of the row layout, gathered from the stage run's planes: per k-slot q one 16-B piece of
+// the row's QS plane entry (dword q of the 4 blocks), its qh dwords (Q5_x) and its f16 scales. In registers
+// (UDW dwords, as the row layout's unit):
+//   [b * QSD + i]  qs dword i of block b (QSD = 4; Q8_0 8: half 1 = dwords 4..7)
+//   [OQH + b]      qh of block b (Q5_0 / Q5_1)
+//   [OD + b / 2]   f16 d of blocks b (low half: even b)      [OM + b / 2] f16 m (Q4_1 / Q5_1)
+// so every block's fields sit at compile-time register indices: no alignbyte, no address arithmetic.
+template <int F, int BPL> struct gemvt_unit {
+    using T = wfmt<F>;
+    static constexpr int QSD = T::Q8 ? 8 : 4;
+    static constexpr int OQH = BPL * QSD;
+    static constexpr int OD = OQH + (T::QH >= 0 ? BPL : 0);
+    static constexpr int OM = OD + BPL / 2;
+    static constexpr int UDW = OM + (T::MOFF >= 0 ? BPL / 2 : 0);
+    static_assert(UDW * 4 == BPL * T::BB, "the unit holds exactly its blocks' bytes");
+};
+
+template <int F, int BI, int BPL> __device__ __forceinline__ wblock decode_block_t(const uint32_t* w) {
+    using T = wfmt<F>;
+    using U = gemvt_unit<F, BPL>;
+    wblock r;
+    r.d = r.m = 0.0f;  // (the dot needs the codes only)
+    if constexpr (T::Q8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.q[i] = w[BI * 8 + i];
+        return r;
+    }
+    uint32_t qh = 0;
+    if constexpr (T::QH >= 0) qh = w[U::OQH + BI];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t v = w[BI * 4 + i];
+        uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+        if constexpr (T::QH >= 0) {
+            lo |= spread4_bit4((qh >> (4 * i)) & 0xFu);
+            hi |= spread4_bit4((qh >> (16 + 4 * i)) & 0xFu);
+        }
+        r.q[i] = lo;
+        r.q[4 + i] = hi;
+    }
+    return r;
+}
+
+// block_dot / block_term_rec of a tiled-layout unit (same arithmetic, same results bit for bit)
+template <int F, int BI, int BPL> __device__ __forceinline__ uint32_t block_dot_t(const uint32_t* w, const uint4 (&a)[3]) {
+    if constexpr (gemv_planes<F>) {
+        const uint32_t l[4] = {a[0].x, a[0].y, a[0].z, a[0].w};
+        const uint32_t h[4] = {a[1].x, a[1].y, a[1].z, a[1].w};
+        uint32_t L = a[2].w;
+        int H = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t q = w[BI * 4 + i];
+            L = __builtin_amdgcn_udot8(q, l[i], L, false);
+            H = __builtin_amdgcn_sdot8((int)(q ^ 0x88888888u), (int)h[i], H, false);
+        }
+        return L + ((uint32_t)H << 4);
+    } else {
+        const wblock wb = decode_block_t<F, BI, BPL>(w);
+        const uint32_t av[8] = {a[0].x, a[0].y, a[0].z, a[0].w, a[1].x, a[1].y, a[1].z, a[1].w};
+        int s = (int)ACC_BIAS;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = __builtin_amdgcn_sdot4((int)wb.q[i], (int)av[i], s, false);
+        return (uint32_t)s;
+    }
+}
+template <int F, int BI, int BPL> __device__ __forceinline__ float block_term_t(const uint32_t* w, uint32_t acc, const uint4& sc) {
+    using U = gemvt_unit<F, BPL>;
+    const float cf = __uint_as_float(acc);
+    const float da = __uint_as_float(sc.x), cs = __uint_as_float(sc.y), nda = __uint_as_float(sc.z);
+    const uint32_t dw = w[U::OD + BI / 2];
+    if constexpr (F == FMT_Q4_0 || F == FMT_Q5_0) {
+        return mixmul<BI & 1>(dw, __builtin_fmaf(da, cf, nda) - cs);
+    } else if constexpr (F == FMT_Q8_0) {
+        return mixmul<BI & 1>(dw, __builtin_fmaf(da, cf, nda));
+    } else {
+        const float fs = cf - ACC_BIAS_F;
+        const float t = mixmul<BI & 1>(dw, da) * fs;
+        return t + mixmul<BI & 1>(w[U::OM + BI / 2], cs);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Load the 32 activation values of block g (AIN_F32: 128 B, AIN_F16_FUSED: 64 B; 16-B aligned).
 template <int AIN> __device__ __forceinline__ void load_act_block(const uint8_t* __restrict__ X, int g, float (&v)[32]) {
     if constexpr (AIN == AIN_F32) {
@@ -195,7 +280,7 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // the rest (output pointer and strides, the sumi hook) is fetched by an s_load that is only waited
 // for at the store, so no kernarg fetch sits in front of the weight stream.
 // (The round-1..4 ablation bits and timeline stamps used to decompose this kernel live in
-// tools/archive/qg_gemv_kernel_r04_knobs.hpp, not here.)
+// profiles/tools_archive/qg_gemv_kernel_r04_knobs.hpp, not here.)
 // The kernel body is shared by two entry points (below): the general one and the M = 1 one with the
 // minimal argument list.
 // TPW (tiles per workgroup, loop-free form only): the workgroup computes TPW consecutive row tiles of
@@ -424,7 +509,7 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // M = 1, one product, out[n] (activation- and weight-major coincide at M = 1): the minimal argument
 // list (A, B, N, K, out) = 8 dwords, all preloaded into SGPRs. Each preloaded kernel-argument dword
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
-// entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
+// entry's 13 preloaded dwords than with these 8 (profiles/tools_archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
 template <int F, int BPL, int LPR, int WGS, bool SUMI, int AIN = AIN_Q8_1, int ONEU = 0>
 __global__ __launch_bounds__(WGS) void gemv1_kernel(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, int N,
@@ -528,12 +613,15 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     const int nu = one ? 1 : !NU_OK ? 0 : nu_all <= 2 ? 2 : nu_all <= 4 ? 4 : 0;
     // M = 1, one product, unit output stride: the minimal-argument entry (gemv1_kernel)
     const bool m1 = MT == 1 && PRE && !NT && g.M == 1 && g.batch == 1 && g.ldc_n == 1;
+    const bool shrt = !m1 && !NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX;
+    // the ONEU the chosen entry launches: the short entry takes the multi-unit form only when
+    // NU_OK && MT > 1, otherwise its loop (ONEU 0) or the one-unit form
+    const int oneu = m1 ? nu : shrt ? ((nu > 1 && !(NU_OK && MT > 1)) ? 0 : nu) : (int)one;
     if (g.group && (SUMI || AIN != AIN_Q8_1 || NT || MT > 4)) return hipErrorInvalidValue;  // no grouped form here
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
         describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
-                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), (m1 || (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX)) ? nu : (int)one,
-                        m1 ? "m1" : (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) ? "short" : "full", grid,
-                        g.batch);
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), oneu, m1 ? "m1" : shrt ? "short" : "full",
+                        grid, g.batch);
         return hipSuccess;
     }
     if constexpr (!SUMI && AIN == AIN_Q8_1 && !NT && MT <= 4) {  // (AUTO sends only M <= 4 to the GEMV)
@@ -595,7 +683,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
         return hipGetLastError();
     }
     // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)
-    if (!NT && g.batch == 1 && g.ldc_m <= INT32_MAX && g.ldc_n <= INT32_MAX) {
+    if (shrt) {
         auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, 1>
                       : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 0>;
         if constexpr (NU_OK && MT > 1) {

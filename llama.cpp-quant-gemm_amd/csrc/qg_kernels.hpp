@@ -84,15 +84,17 @@ void describe_kernel(const GemmArgs& g, const char* fmt, ...);
 bool gemv_eligible(const GemmArgs& g);
 hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
 
+// The decode GEMV (M <= 4) on the tiled layout (qg_gemvt.hip, round 6): waves of 16 rows x 4 stages reading
+// whole 256-B plane runs, the row kernel's dot and per-block terms (bit-identical per block to the
+// reference's), fixed summation order.
+bool gemvt_eligible(const GemmArgs& g);
+hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st);
+
 // Prefill (M >= 5): LDS-DMA staged weights + activations, one v_mfma_i32_16x16x32_i8 per Q-block,
 // MFMA-assisted (v_mfma_f32_16x16x16_f16) scale epilogue.
 bool mfma_eligible(const GemmArgs& g);
 hipError_t launch_mfma(const GemmArgs& g, hipStream_t st);
 
-// The decode GEMV (M <= 4) on the tiled layout (qg_gemvt.hip): per-block terms bit-identical to the
-// reference's, fixed summation order.
-bool gemvt_eligible(const GemmArgs& g);
-hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st);
 
 // Any shape / alignment with K % 32 == 0 (byte-granular loads); also the debug sumi fallback.
 hipError_t launch_generic(const GemmArgs& g, hipStream_t st);

@@ -2,7 +2,7 @@
 // (qg_mmq_kernel.hpp), instantiated once per weight format (qg_mmq_q*.hip) so the formats compile in
 // parallel; qg_gemm_mfma.hip switches on the format.
 //
-// Tile configuration from the sweeps in tools/archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
+// Tile configuration from the sweeps in profiles/tools_archive/mmq_probe.hip (profiles/r01_tuning/mmq_probe6.txt,
 // mmq_probe_smallm.txt; cold weights, one MI355X):
 //  * M <= 32: 16 tokens per workgroup, 8 waves splitting K; 32 weight rows when that still gives
 //    >= 256 workgroups (one per CU; fewer re-reads of the activations), else 16
@@ -11,16 +11,16 @@
 //    4 (two workgroups per CU under the kernel's register cap; mmq_probe_p4.txt, mmq_probe_mid.txt,
 //    mmq_probe_lb.txt: M=64 10.1 us, M=128 15.2 us, M=512 47 us with the MFMA-assisted epilogue)
 //  * round 4, measured and not adopted: the whole K of a 32 x 16 tile resident in LDS with every
-//    operand byte requested at entry and a barrier per 32-block phase (tools/archive/
+//    operand byte requested at entry and a barrier per 32-block phase (profiles/tools_archive/
 //    mmqr_resident_experiment.hpp; profiles/r04_tuning/ab_mmqr.txt: M = 32 6.91 -> 8.35 us, M = 24
 //    6.72 -> 8.20, N = 11008 14.7 -> 21.3; parity green) — with everything in flight no phase completes
 //    until most bytes have landed, so the compute no longer overlaps the ingest.
 //  * round 4, measured and not adopted: a chunked, workgroup-cooperative ingest (576-B row segments
-//    instead of 72 B, one barrier per 32-block chunk; tools/archive/mmqc_experiment.hpp,
+//    instead of 72 B, one barrier per 32-block chunk; profiles/tools_archive/mmqc_experiment.hpp,
 //    profiles/r04_tuning/ab_mmqc_v1.txt: M = 32 6.91 -> 8.54 us, N = 11008 14.7 -> 22.3), early refill
 //    of consumed stage buffers (ab_early.txt: M = 32 6.90 -> 7.14 us), raw fragment batches (ab_raw.txt),
 //    dynamic stage hand-out (profiles/r02_tuning/ab_dyn.txt: M = 32 6.87 -> 7.25 us); their code is in
-//    tools/archive/qg_mmq_kernel_r04_knobs.hpp.
+//    profiles/tools_archive/qg_mmq_kernel_r04_knobs.hpp.
 // The same configurations serve every weight layout (LAY_ROWS, LAY_TILED) and the activation-window
 // form (AW: odd K/32 against stage-padded weights).
 #pragma once

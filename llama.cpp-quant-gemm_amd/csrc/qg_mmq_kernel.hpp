@@ -53,7 +53,7 @@
 // first prompted it came from an MFMA result element read through a bit_cast, mmq_probe1-2.txt).
 // Only LDS reads in the main loop: an LDS write there makes hipcc wait for every DMA in flight.
 // (Rejected round-4 tuning forms — early refill, raw fragment batches, dynamic stage hand-out,
-// ablations, timeline stamps — live in tools/archive/qg_mmq_kernel_r04_knobs.hpp, not here.)
+// ablations, timeline stamps — live in profiles/tools_archive/qg_mmq_kernel_r04_knobs.hpp, not here.)
 #pragma once
 #include "qg_common.hpp"
 #include "qg_kernels.hpp"
@@ -233,7 +233,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     // All lanes issue every DMA instruction (lanes past the image fetch a clamped piece into the
     // padding): a lane-predicated global_load_lds let hipcc sink two of them into one block with a
     // per-lane M0 base, read back with v_readfirstlane — wrong destinations for half the wave
-    // (found by tools/archive/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
+    // (found by profiles/tools_archive/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = TL ? Bw + (long)h * TF::STG : Bw + (long)h * G::RSB - G::shift(h);
         const uint8_t* asrc = Aw + (long)h * (G::TA ? ACT_STG : MMQ_SB * Q8_1_BYTES);

@@ -3,7 +3,7 @@
 // With K/32 odd, every other weight row starts 2 bytes off a dword, which the MFMA kernel's LDS-DMA
 // pieces cannot address; the ragged kernel (qg_ragged.hip) serves those shapes with one wave per
 // weight row and no matrix cores (K = 4128: 24.6 us at M = 32, 45.9 us at M = 64 against 6-9 us for
-// the MFMA kernel on the same bytes; tools/archive/repack_probe.py, profiles/r02_tuning/repack_probe.txt).
+// the MFMA kernel on the same bytes; profiles/tools_archive/repack_probe.py, profiles/r02_tuning/repack_probe.txt).
 // Here one streaming kernel copies the weights [N][K/32] and the activations [M][K/32] into rows of
 // K'/32 = round_up(K/32, 8) blocks in a per-stream workspace, the extra blocks all zero bytes
 // (d = 0 and s = 0: each padded term of gemm_reference.h:202-212 is an exact +0), and the MFMA

@@ -86,22 +86,19 @@ int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, in
     const size_t count = (size_t)M * (size_t)P;
     hipStream_t st = (hipStream_t)stream;
     const bool in_place = M == 1 && N % world == 0;
+    const size_t need = qg_sharded_gemm_workspace_size(M, N, world);
+    const bool ws_ok = in_place || (ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0);
+    // A missing or short workspace where the gather buffer does not fit in C (N % world != 0) is reported
+    // before anything is enqueued: its size depends only on (M, N, world), which every rank shares, so a
+    // caller passing the workspace alike on every rank gets this error on every rank (none waits).
+    if (!ws_ok && N % world != 0) return QG_ERR_UNSUPPORTED;
     // From here on a failure is RANK-LOCAL (this rank's shard pointer, its workspace, its kernel): the rank
     // still takes part in the one collective — with its slice set to NaN — and returns the error after it,
-    // so its peers complete the all-gather (and see NaN columns) instead of blocking in it.
-    int local_rc = QG_OK;
-    float* recv = C;
-    void* tmp = nullptr;
-    if (!in_place) {
-        const size_t need = qg_sharded_gemm_workspace_size(M, N, world);
-        if (ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0) {
-            recv = static_cast<float*>(ws);
-        } else {  // a receive buffer for the collective only; the call fails
-            local_rc = QG_ERR_UNSUPPORTED;
-            if (hipMallocAsync(&tmp, need, st) != hipSuccess) return QG_ERR_HIP;  // cannot take part at all
-            recv = static_cast<float*>(tmp);
-        }
-    }
+    // so its peers complete the all-gather (and see NaN columns) instead of blocking in it. The error path
+    // allocates nothing: without a usable workspace (N % world == 0 here) the world * M * P =
+    // M * N floats of the gather land in C itself, which is then set to NaN.
+    int local_rc = ws_ok ? QG_OK : QG_ERR_UNSUPPORTED;
+    float* recv = in_place || !ws_ok ? C : static_cast<float*>(ws);
     float* mine = recv + (size_t)rank * count;
     if (local_rc == QG_OK && rows > 0 && !B_shard) local_rc = QG_ERR_INVALID_ARG;
     if (local_rc == QG_OK) local_rc = qg_sharded_gemm_w4a8_local(A, B_shard, mine, M, N, K, wtype, world, rank, stream);
@@ -113,7 +110,8 @@ int qg_sharded_gemm_w4a8(const void* A, const void* B_shard, float* C, int M, in
                            (const float*)recv, C, M, N, (int)P);
         if (hipGetLastError() != hipSuccess) rc = QG_ERR_HIP;
     }
-    if (tmp) (void)hipFreeAsync(tmp, st);
+    // the failing rank's own C: all NaN (its slice never reached its peers as numbers either)
+    if (local_rc != QG_OK) (void)hipMemsetD32Async(C, 0x7FC00000, (size_t)M * N, st);
     return local_rc != QG_OK ? local_rc : rc;
 }
 

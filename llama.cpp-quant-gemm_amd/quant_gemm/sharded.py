@@ -109,11 +109,35 @@ class RowShardedW4A8:
         return gathered.permute(1, 0, 2).reshape(M, world * rows)[:, :n_total]
 
     def forward(self, act_q: torch.Tensor, M: int) -> torch.Tensor:
+        """C[M, n_total] on every rank. Collective safety (as libqg_shard.so, include/qg/qg_shard.h): a
+        failure of this rank's own compute does not skip the all-gather — the rank contributes a quiet-NaN
+        slice, takes part in the collective and raises ShardComputeError afterwards, so its peers return
+        (with NaN in this rank's columns, ``failed_ranks`` names them) instead of waiting forever."""
         out = self.local_out(M)
-        self.compute_local(act_q, M, out)
+        err = None
+        try:
+            self.compute_local(act_q, M, out)
+        except Exception as e:  # noqa: BLE001  (any rank-local failure: re-raised after the collective)
+            out.fill_(float("nan"))
+            err = e
         g = self.gather_buffer(M)
         self.gather(out, g)
+        if err is not None:
+            raise ShardComputeError(f"rank {self.rank}: local compute failed ({err!r}); its slice was sent as NaN") from err
         return self.assemble(g, self.n_total)
+
+    def failed_ranks(self, C: torch.Tensor) -> list:
+        """Ranks whose columns of a forward() result are NaN (a peer's rank-local failure)."""
+        bad = []
+        for r in range(self.world):
+            s0, s1 = shard_rows(self.n_total, self.world, r)
+            if s1 > s0 and bool(torch.isnan(C[:, s0:s1]).all()):
+                bad.append(r)
+        return bad
+
+
+class ShardComputeError(RuntimeError):
+    """This rank's own part of a sharded product failed; the collective still ran (peers hold NaN)."""
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1,6 +1,6 @@
 // qg_gemv_kernel.hpp — the W4A8 GEMV / small-batch kernels (M <= 8 activation rows).
 //
-// Included by qg_gemv.hip (the product's instantiations + dispatch) and by tools/archive/gemv_probe.hip
+// Included by qg_gemv.hip (the product's instantiations + dispatch) and by profiles/tools_archive/gemv_probe.hip
 // (the tuning sweep). Computes, for the reference's activation-major contract
 // C[M,N] = A_q8_1[M,K] . B_w[N,K]^T (include/gemm_reference.h:175-222):
 //   C[m*ldc_m + n*ldc_n] = sum_b term(A[m][b], B[n][b]).
@@ -47,7 +47,7 @@
 namespace qg {
 
 #ifdef QG_STAMPS
-// diagnostic build only (tools/archive/timeline_probe.hip; never in the product build): per wave 8 slots: 100-MHz stamps at entry,
+// diagnostic build only (profiles/tools_archive/timeline_probe.hip; never in the product build): per wave 8 slots: 100-MHz stamps at entry,
 // after the activation barrier, weights landed, compute done, exit; s_memtime at entry and exit;
 // (XCC_ID << 32 | HW_ID)
 __device__ unsigned long long g_stamps[8 * 65536];
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(WGS) void gemvs_kernel(const uint32_t* __restrict__
 // M = 1, one product, out[n] (activation- and weight-major coincide at M = 1): the minimal argument
 // list (A, B, N, K, out) = 8 dwords, all preloaded into SGPRs. Each preloaded kernel-argument dword
 // costs every wave's launch: the single-launch M = 1 GEMV took 0.11 us longer with the general
-// entry's 13 preloaded dwords than with these 8 (tools/archive/gemv_direct_probe.hip,
+// entry's 13 preloaded dwords than with these 8 (profiles/tools_archive/gemv_direct_probe.hip,
 // profiles/r02_tuning/gemv_abl*.txt). SUMI: out is the parity hook's int32 buffer.
 #ifndef QG_GEMV_WGSTORE
 #define QG_GEMV_WGSTORE 0

@@ -56,7 +56,7 @@ constexpr float MMQ_BIAS_F = 12582912.0f;
 constexpr int MMQ_SB = 4;             // blocks per compute sub-stage (a DMA stage holds SB = 4 or 8)
 
 #ifdef QG_MMQ_STAMPS
-// diagnostic build only (tools/archive/mmq_timeline.hip): per-wave s_memrealtime stamps
+// diagnostic build only (profiles/tools_archive/mmq_timeline.hip): per-wave s_memrealtime stamps
 __device__ unsigned long long g_mmq_stamps[8 * 65536];
 #define MMQ_STAMP(k) stamps[k] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -246,7 +246,7 @@ __device__ __forceinline__ void mmq_body(const uint8_t* __restrict__ A, const ui
     // All lanes issue every DMA instruction (lanes past the image fetch a clamped piece into the
     // padding): a lane-predicated global_load_lds let hipcc sink two of them into one block with a
     // per-lane M0 base, read back with v_readfirstlane — wrong destinations for half the wave
-    // (found by tools/archive/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
+    // (found by profiles/tools_archive/mmq_debug.hip on Q4_1, 16 rows x 16 tokens).
     auto issue = [&](int h, uint8_t* buf) {
         const uint8_t* wsrc = Bw + (long)h * G::RSB - G::shift(h);
         const uint8_t* asrc = Aw + (long)h * (SB * Q8_1_BYTES);

@@ -55,6 +55,22 @@ def test_baseline_q4_0_m32_tiled_full_size(O, qg, m, n, k):
     assert O.nmse(c, O.gemm_fp32(a, b)) <= 5e-3
 
 
+@pytest.mark.parametrize("m,n,k", [(1, 4096, 4096), (1, 4096, 14336), (4, 4096, 14336)])
+def test_baseline_q4_0_decode_tiled_full_size(O, qg, m, n, k):
+    """BASELINE configs[1] (and the published 4096 x M x 14336 decode shapes) on the tiled layout: the tiled
+    decode GEMV (round 6) — sumi bit-exact per block through the instantiation the
+    product launches, outputs within the summation-order bound of the oracle, NMSE <= 5e-3."""
+    a, b, aq, bq = make_case(O, m, n, k, 2)
+    bt = qg.tile_weights(dev(bq), n, k, 2)
+    cfg = qg.debug_config_tiled(m, n, k, 2)
+    assert cfg == qg.debug_config_tiled(m, n, k, 2, sumi=True) and cfg.startswith(f"gemvt F=2 MT={m} "), cfg
+    c_ref, want = O.gemm_w4a8(aq, bq, 2, want_sumi=True)
+    assert np.array_equal(host(qg.debug_sumi_tiled(dev(aq), bt, m, n, k, 2)), want)
+    c = host(qg.gemm_w4a8_tiled(dev(aq), bt, m, n, k, 2))
+    assert (np.abs(c.astype(np.float64) - c_ref) <= O.summation_tol(aq, bq, want, 2)).all()
+    assert O.nmse(c, O.gemm_fp32(a, b)) <= 5e-3
+
+
 # bounds just above the oracle's NMSE on this recipe (4.5550e-3, 3.7749e-3, 1.0032e-3, 8.7440e-4 with
 # the include/quantize.h Q8_1 quantizer; the reference-compiled values with the test_framework one,
 # tests/golden/kat.json, are asserted on the oracle in tests/test_oracle.py)

@@ -64,3 +64,30 @@ def test_native_local_slice_matches_columns(O, qg):
         got = host(out)
         assert np.array_equal(got[:, : s1 - s0], full[:, s0:s1])
         assert np.isnan(got[:, s1 - s0:]).all()  # padding columns untouched
+
+
+def test_native_rank_local_errors_join_the_collective(O, qg, comm):
+    """The error paths of qg_sharded_gemm_w4a8 allocate nothing and still run the one all-gather:
+    M > 1 without a workspace (N % world == 0: the gather lands in C) and a null shard with rows to compute
+    return their error with C all NaN; the stream stays usable and the next good call is exact."""
+    import ctypes
+
+    import torch
+    from quant_gemm.sharded import NativeRowShardedW4A8, shard_lib
+    m, n, k = 3, 512, 1024
+    _, _, aq, bq = make_case(O, m, n, k, 2)
+    a_d, b_d = dev(aq), dev(bq)
+    lib = shard_lib()
+    P = ctypes.c_void_p
+    st = P(torch.cuda.current_stream().cuda_stream)
+    c = torch.zeros((m, n), dtype=torch.float32, device="cuda")
+    assert lib.qg_sharded_gemm_w4a8(P(a_d.data_ptr()), P(b_d.data_ptr()), P(c.data_ptr()), m, n, k, 2, None, 0,
+                                    comm.handle, st) == -3  # QG_ERR_UNSUPPORTED: no workspace
+    assert torch.isnan(c).all()
+    c.zero_()
+    ws = torch.empty(lib.qg_sharded_gemm_workspace_size(m, n, 1) // 4, dtype=torch.float32, device="cuda")
+    assert lib.qg_sharded_gemm_w4a8(P(a_d.data_ptr()), None, P(c.data_ptr()), m, n, k, 2, P(ws.data_ptr()),
+                                    ws.numel() * 4, comm.handle, st) == -1  # QG_ERR_INVALID_ARG: null shard
+    assert torch.isnan(c).all()
+    good = NativeRowShardedW4A8(b_d, n, k, comm).forward(a_d, m)
+    assert np.array_equal(host(good), host(qg.gemm_w4a8(a_d, b_d, m, n, k)))

@@ -1,7 +1,7 @@
 """The M <= 32 prefill at wide-row shapes (>= 256 tiles of 32 rows x 16 tokens: the 32-row MFMA tile
 of BASELINE configs[2]): full-size configs[2] for every weight format, ragged M / N edges at that tile,
 K from one to 160 blocks, raw random bytes, strided outputs and repeat determinism. (Written in round 4
-for a chunked-ingest variant of the kernel, tools/archive/mmqc_experiment.hpp, measured slower and not
+for a chunked-ingest variant of the kernel, profiles/tools_archive/mmqc_experiment.hpp, measured slower and not
 shipped; the cases stay as parity coverage of the product tile.) Bars as in test_gpu_parity.py: per-block int32
 sumi bit-exact through the parity hook (the same instantiation), outputs within oracle.reassoc_tol
 (DESIGN.md §5). Oracle contract: include/gemm_reference.h:175-222."""
