@@ -627,9 +627,14 @@ def compact_summary(out: dict) -> dict:
         sm[f"cpu_{x.get('cores')}t_ms"] = x.get("ms_per_gemv")
     if out.get("strong"):
         sm["strong"] = {k: v for k, v in out["strong"].items() if "speedup" in k}
+    # "[wtype:]MxNxK:form=us": wtype omitted for q4_0; forms s(ingle) t(iled) ta (tiled_act) b(atched, per
+    # GEMV) pp (prepacked) pd (padded) w16; fractions of HBM / the i8 peak follow from the bytes and flops
+    ab = {"single": "s", "tiled": "t", "tiled_act": "ta", "batched": "b", "prepacked": "pp", "padded": "pd", "w16": "w16"}
     rows = []
     for c in out.get("side_configs") or []:
-        rows.append(f"{c['wtype']}/{c['M']}x{c['N']}x{c['K']}/{c['form']}={c['us_per_launch']}@{c.get('frac_hbm')}")
+        us = c.get("us_per_launch", c.get("us_per_gemv"))  # (the batched form's rows are per GEMV)
+        w = "" if c["wtype"] == "q4_0" else c["wtype"] + ":"
+        rows.append(f"{w}{c['M']}x{c['N']}x{c['K']}:{ab.get(c['form'], c['form'])}={us}")
     sm["side"] = rows
     return sm
 

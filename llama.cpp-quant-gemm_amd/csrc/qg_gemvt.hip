@@ -27,12 +27,16 @@ namespace qg {
 
 namespace {
 
-// tuning (A/B builds): rows per wave (16: the half tile, 4 stage lanes; 8: 8 stage lanes) and stages per lane
+// tuning (A/B builds): rows per wave (16: the half tile, 4 stage lanes; 8: 8 stage lanes; 0: per shape, below)
+// and stages per lane
 #ifndef QG_GEMVT_R
-#define QG_GEMVT_R 16
+#define QG_GEMVT_R 0
 #endif
 #ifndef QG_GEMVT_NU
 #define QG_GEMVT_NU 0  // 0: per K (gemvt_nu below)
+#endif
+#ifndef QG_GEMVT_RED
+#define QG_GEMVT_RED 0  // cross-wave sum: 0 after a workgroup barrier (wave 0 sums), 1 by the last wave to finish
 #endif
 #ifndef QG_GEMVT_ABL
 #define QG_GEMVT_ABL 0  // (A/B ablation builds only) 1: no cross-wave sum, 2: no staging, 4: no dot
@@ -109,6 +113,13 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
         }
     }
 
+    if (QG_GEMVT_RED == 1 && !SUMI) {
+        // the last-arriver counter of the cross-wave sum: zeroed, then one barrier while the loads are in
+        // flight (LDS writes drained, no wait on the global loads)
+        if (threadIdx.x == 0) lds[W * (NU * SL) * RSTR + MT * W * R] = 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+
     // 2) the wave's records: item it -> stage-local block jb = 4 jl + b, token m, at jl * RSTR + (b MT + m) * 12
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
@@ -126,43 +137,49 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // 3) dots and per-block terms, unit by unit, block by block
+    // 3) dots and per-block terms, unit by unit, block by block. The records of step i = (unit j, block b)
+    //    are read PD steps ahead (all of unit 0 before the first weight byte is waited for), so the LDS
+    //    latency sits under the weight stream instead of between the dots of the tail (4.16 -> 4.07 us at
+    //    M = 1, N = K = 4096; K = 14336 8.94 -> 7.76 with 2 stages per lane).
+    constexpr int NS = NU * GT_SB;
+    // (within the 128 VGPRs of a 1024-thread workgroup; the byte-decode formats need more for the dot)
+    constexpr int PD = MT == 1 ? 4 : MT == 2 ? (gemv_planes<F> ? 2 : 1) : 0;
+    constexpr int RB = PD + 1;  // ring of record slots (compile-time indices: registers, not scratch)
+    uint4 rb[RB][MT][3];
+    auto rd = [&](auto IC) {
+        constexpr int i = decltype(IC)::value;
+        if constexpr (i < NS) {
+            const uint32_t* rec = wl + ((i / GT_SB) * SL + s) * RSTR + (i % GT_SB) * MT * 12;
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int x = 0; x < 3; ++x) rb[i % RB][m][x] = *reinterpret_cast<const uint4*>(rec + m * 12 + 4 * x);
+        }
+    };
+    static_for<PD>([&](auto IC) { rd(IC); });
+    __builtin_amdgcn_sched_barrier(0);
     float acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = 0.0f;
+    static_for<NS>([&](auto IC) {
+        constexpr int i = decltype(IC)::value, j = i / GT_SB, b = i % GT_SB;
+        rd(ic<i + PD>{});
+        const int h = h0 + j * SL + s;
 #pragma unroll
-    for (int j = 0; j < NU; ++j) {
-        const int jl = j * SL + s, h = h0 + jl;
-        const uint32_t* rec0 = wl + jl * RSTR;
-        static_for<GT_SB>([&](auto BI) {
-            constexpr int b = decltype(BI)::value;
-#pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                if (m < M) {
-                    const uint32_t* rec = rec0 + (b * MT + m) * 12;
-                    uint4 a[3];
-                    if (QG_GEMVT_ABL & 2) {
-                        a[0] = a[1] = make_uint4(0x11111111u * (m + 1), 0x01010101u, 0x22222222u, 0x03030303u);
-                        a[2] = make_uint4(0x3c000000u, 0x3c000000u, 0xbc000000u, ACC_BIAS);
-                    } else {
-                        a[0] = *reinterpret_cast<const uint4*>(rec);
-                        a[1] = *reinterpret_cast<const uint4*>(rec + 4);
-                        a[2] = *reinterpret_cast<const uint4*>(rec + 8);
-                    }
-                    uint32_t d;
-                    if (QG_GEMVT_ABL & 4) d = wu[j][b] ^ wu[j][4 + b] ^ wu[j][TU::OD];
-                    else d = block_dot_t<F, b, GT_SB>(wu[j], a);
-                    const int gb = h * GT_SB + b;
-                    if constexpr (SUMI) {
-                        if (n < N && h < H && gb < nb) static_cast<int32_t*>(out)[((long)m * N + n) * nb + gb] = (int)(d - ACC_BIAS);
-                    } else {
-                        const float t = (QG_GEMVT_ABL & 4) ? __uint_as_float(d) : block_term_t<F, b, GT_SB>(wu[j], d, a[2]);
-                        if (h < H) acc[m] += t;
-                    }
+        for (int m = 0; m < MT; ++m) {
+            if (m < M) {
+                const uint4 a[3] = {rb[i % RB][m][0], rb[i % RB][m][1], rb[i % RB][m][2]};
+                const uint32_t d = block_dot_t<F, b, GT_SB>(wu[j], a);
+                const int gb = h * GT_SB + b;
+                if constexpr (SUMI) {
+                    if (n < N && h < H && gb < nb) static_cast<int32_t*>(out)[((long)m * N + n) * nb + gb] = (int)(d - ACC_BIAS);
+                } else {
+                    const float t = block_term_t<F, b, GT_SB>(wu[j], d, a[2]);
+                    if (h < H) acc[m] += t;
                 }
             }
-        });
-    }
+        }
+    });
     if constexpr (!SUMI) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<SL>(acc[m]);
@@ -181,6 +198,24 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
 #pragma unroll
             for (int m = 0; m < MT; ++m) red[(m * W + wave) * R + r] = acc[m];
         }
+        if (QG_GEMVT_RED == 1) {
+            // the last wave to arrive sums: a wave's LDS operations execute in order, so when its counter
+            // add returns W - 1 every other wave's partials are in LDS (no workgroup barrier)
+            uint32_t* cnt = reinterpret_cast<uint32_t*>(red + MT * W * R);
+            uint32_t prev = 0;
+            if (lane == 0) prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            prev = __builtin_amdgcn_readfirstlane(prev);
+            if (prev != (uint32_t)(W - 1)) return;
+            if (lane < R * MT) {
+                const int m = lane / R, rw = lane % R, nn = tile * R + rw;
+                if (m < M && nn < N) {
+                    float v = red[m * W * R + rw];
+                    for (int w = 1; w < W; ++w) v += red[(m * W + w) * R + rw];
+                    static_cast<float*>(out)[(long)m * ldc_m + (long)nn * ldc_n] = v;
+                }
+            }
+            return;
+        }
         __syncthreads();
         const int tid = threadIdx.x;
         if (tid < R * MT) {
@@ -194,22 +229,24 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
     }
 }
 
-// stages per lane: enough waves per workgroup to fill a CU without more than 16, units in flight per lane
-template <int F> int gemvt_nu(int H) {
-    if (QG_GEMVT_NU) return QG_GEMVT_NU;
-    constexpr int SL = 64 / QG_GEMVT_R;
-    constexpr int numax = (F == FMT_Q8_0 || F == FMT_Q5_1) ? 2 : 4;  // VGPRs of the larger units
-    int nu = 1;
-    while (nu < numax && (H + nu * SL - 1) / (nu * SL) > 8) nu *= 2;
-    return nu;
+// Rows per wave and stages per lane (profiles/r06_tuning/r6g_ab.txt, N = 4096): 8 rows x 8 stages for M <= 2
+// up to K = 4096 (M = 1 4.02 -> 3.83 us, M = 2 4.35 -> 4.13; worse at M = 4 and long K), else the half tile x 4
+// stages; 1 stage per lane while 8 waves cover the row group's stages, else 2 (K = 14336 8.94 -> 7.76 us
+// against 4 per lane; at most 16 waves: K <= 16384).
+struct gemvt_shape {
+    int R, NU;
+};
+inline gemvt_shape gemvt_pick(int M, int H) {
+    const int R = QG_GEMVT_R ? QG_GEMVT_R : (M <= 2 && H <= 32) ? 8 : 16, SL = 64 / R;
+    return {R, QG_GEMVT_NU ? QG_GEMVT_NU : (H + SL - 1) / SL > 8 ? 2 : 1};
 }
 
-template <int F, int MT, int NU> hipError_t gemvt_launch(const GemmArgs& g, hipStream_t st) {
-    constexpr int R = QG_GEMVT_R, SL = 64 / R;
+template <int F, int MT, int R, int NU> hipError_t gemvt_launch(const GemmArgs& g, hipStream_t st) {
+    constexpr int SL = 64 / R;
     const int nb = g.K / QK, H = (nb + GT_SB - 1) / GT_SB;
     const int W = (H + NU * SL - 1) / (NU * SL);
     const int grid = (g.N + R - 1) / R;
-    const size_t lds = ((size_t)W * NU * SL * (48 * MT + 4) + (size_t)W * R * MT) * 4;
+    const size_t lds = ((size_t)W * NU * SL * (48 * MT + 4) + (size_t)W * R * MT + 4) * 4;
     const bool ta = g.lay == LAY_TILED_ACT;
     if (g.describe) {
         describe_kernel(g, "gemvt F=%d MT=%d R=%d NU=%d W=%d TA=%d grid=%d", F, MT, R, NU, W, (int)ta, grid);
@@ -230,14 +267,9 @@ template <int F, int MT, int NU> hipError_t gemvt_launch(const GemmArgs& g, hipS
 }
 
 template <int F, int MT> hipError_t gemvt_m(const GemmArgs& g, hipStream_t st) {
-    const int H = (g.K / QK + GT_SB - 1) / GT_SB;
-    switch (gemvt_nu<F>(H)) {
-        case 1: return gemvt_launch<F, MT, 1>(g, st);
-        case 2: return gemvt_launch<F, MT, 2>(g, st);
-        default:
-            if constexpr (F == FMT_Q8_0 || F == FMT_Q5_1) return gemvt_launch<F, MT, 2>(g, st);
-            else return gemvt_launch<F, MT, 4>(g, st);
-    }
+    const gemvt_shape p = gemvt_pick(g.M, (g.K / QK + GT_SB - 1) / GT_SB);
+    if (p.R == 8) return p.NU == 1 ? gemvt_launch<F, MT, 8, 1>(g, st) : gemvt_launch<F, MT, 8, 2>(g, st);
+    return p.NU == 1 ? gemvt_launch<F, MT, 16, 1>(g, st) : gemvt_launch<F, MT, 16, 2>(g, st);
 }
 
 template <int F> hipError_t gemvt_f(const GemmArgs& g, hipStream_t st) {
@@ -251,22 +283,18 @@ template <int F> hipError_t gemvt_f(const GemmArgs& g, hipStream_t st) {
 }  // namespace
 
 // M <= 4, one product with 32-bit output strides; B_tiled 16-B aligned, A 4-B aligned; at most 16 waves
-// per workgroup (K/32 <= 16 waves x 4 stage lanes x NU stages x 4 blocks: K <= 131072 for Q4_0).
+// per workgroup (K/32 <= 16 waves x 4 stage lanes x 2 stages x 4 blocks: K <= 16384). Beyond, run_tiled takes
+// the MFMA kernel.
 bool gemvt_eligible(const GemmArgs& g) {
     if (!(g.lay == LAY_TILED || g.lay == LAY_TILED_ACT) || g.M < 1 || g.M > 4 || g.N < 1 || g.K % QK != 0) return false;
     if (g.batch != 1 || g.group || g.ain != AIN_Q8_1 || ((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 3) != 0) return false;
     if (g.ldc_m > INT32_MAX || g.ldc_n > INT32_MAX || g.ldc_m < 0 || g.ldc_n < 0) return false;
-    const int H = (g.K / QK + GT_SB - 1) / GT_SB, SL = 64 / QG_GEMVT_R;
-    int nu = 0;
-    switch (g.wtype) {
-        case FMT_Q4_0: nu = gemvt_nu<FMT_Q4_0>(H); break;
-        case FMT_Q4_1: nu = gemvt_nu<FMT_Q4_1>(H); break;
-        case FMT_Q5_0: nu = gemvt_nu<FMT_Q5_0>(H); break;
-        case FMT_Q5_1: nu = gemvt_nu<FMT_Q5_1>(H); break;
-        case FMT_Q8_0: nu = gemvt_nu<FMT_Q8_0>(H); break;
-        default: return false;
-    }
-    return (H + nu * SL - 1) / (nu * SL) <= 16 && (long)g.M * g.N * (g.K / QK) < (1L << 62);
+    if (!(g.wtype == FMT_Q4_0 || g.wtype == FMT_Q4_1 || g.wtype == FMT_Q5_0 || g.wtype == FMT_Q5_1 || g.wtype == FMT_Q8_0))
+        return false;
+    const int H = (g.K / QK + GT_SB - 1) / GT_SB;
+    const gemvt_shape p = gemvt_pick(g.M, H);
+    const int SL = 64 / p.R;
+    return (H + p.NU * SL - 1) / (p.NU * SL) <= 16 && (long)g.M * g.N * (g.K / QK) < (1L << 62);
 }
 
 hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st) {

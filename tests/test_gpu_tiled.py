@@ -34,10 +34,10 @@ SHAPES = [
     (1, 4096, 4096),   # configs[1] on the tiled layout: the tiled decode GEMV (round 6: 16 rows x 4 stages per wave)
     (1, 300, 4128),    # decode GEMV, odd K/32 (padding blocks), ragged N
     (1, 32000, 1024),  # decode GEMV, many row tiles (linear order)
-    (1, 4096, 14336),  # decode GEMV, 4 stages per lane (2 for Q5_1 / Q8_0), 7 / 14 waves
+    (1, 4096, 14336),  # decode GEMV, 2 stages per lane, 14 waves
     (4, 300, 4128),    # M = 2..4: the tiled decode GEMV too, padding blocks
     (3, 32000, 1024),  # M = 2..4, many row tiles (linear order)
-    (2, 4096, 14336),  # M = 2, several stages per lane
+    (2, 4096, 14336),  # M = 2, 2 stages per lane
     (4, 64, 160),      # one wave per workgroup (no cross-wave sum), stages past K/32
     (32, 4096, 4096),  # configs[2]: 32 x 16 tiles, 12 waves, one dispatch round
     (5, 4096, 4096),   # 16-row tiles
