@@ -288,6 +288,9 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
+#ifndef QG_GEMV_ACT2
+#define QG_GEMV_ACT2 1  // (A/B builds) 0: M >= 2 loads each further activation block after the previous record
+#endif
 template <int F, int MT, int BPL, int LPR, int WGS, bool SUMI, int AIN, bool NT, bool PRE, int ONEU, int TPW = 1>
 __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const uint8_t* __restrict__ B, long sA, long sB,
                                           int M, int N, int K, float* __restrict__ C, long sC, long ldc_m, long ldc_n,
@@ -360,17 +363,25 @@ __device__ __forceinline__ void gemv_body(const uint32_t* __restrict__ A, const 
     //    weight stream; 2) the lane's first weight unit; 3) LDS records
     const int totb = M * nb;
     if constexpr (AIN == AIN_Q8_1) {
-        uint32_t ab[9];
-        auto load_ablk = [&](int g) {
+        // M >= 2: a thread's first TWO blocks are loaded before the weight stream (M = 4 at K = 14336 stages
+        // 1792 blocks over 1024 threads: the second round no longer waits behind the first one's records)
+        constexpr int NA = MT >= 2 && QG_GEMV_ACT2 ? 2 : 1;
+        uint32_t ab[NA][9];
+        auto load_ablk = [&](int g, uint32_t (&d)[9]) {
             const uint32_t* p = A + (long)g * 9;
 #pragma unroll
-            for (int i = 0; i < 9; ++i) ab[i] = p[i];
+            for (int i = 0; i < 9; ++i) d[i] = p[i];
         };
-        if (tid < totb) load_ablk(tid);
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (tid + k * WGS < totb) load_ablk(tid + k * WGS, ab[k]);
         load_first();
-        for (int g = tid; g < totb; g += WGS) {
-            if (g != tid) load_ablk(g);
-            make_act_record<F>(ab, lds + rec_of(g));
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (tid + k * WGS < totb) make_act_record<F>(ab[k], lds + rec_of(tid + k * WGS));
+        for (int g = tid + NA * WGS; g < totb; g += WGS) {
+            load_ablk(g, ab[0]);
+            make_act_record<F>(ab[0], lds + rec_of(g));
         }
     } else {
         const uint8_t* X = reinterpret_cast<const uint8_t*>(A);
