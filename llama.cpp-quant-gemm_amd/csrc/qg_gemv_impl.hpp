@@ -19,6 +19,9 @@
 #ifndef QG_GEMV_SMALLK
 #define QG_GEMV_SMALLK 1  // K < 4096 shapes on 16-row workgroups (0: the round-2 64-row form, A/B builds)
 #endif
+#ifndef QG_GEMVM_LPR
+#define QG_GEMVM_LPR 64
+#endif
 #ifndef QG_GEMVBIG_WGS
 #define QG_GEMVBIG_WGS 512
 #endif
@@ -54,6 +57,10 @@ hipError_t launch_staged(const GemmArgs& g, hipStream_t st) {
             // 3.93 -> 3.88 us; Q4_0 / Q8_0 are faster at 1024, Q4_1 equal)
             constexpr int W1 = (F == FMT_Q5_0 || F == FMT_Q5_1) ? 512 : QG_GEMV1_WGS;
             if constexpr (MT == 1) if (nb / 2 <= 64) return gemv_launch<F, MT, 2, 64, W1, SUMI, AIN, false, true>(g, st);
+#if QG_GEMVM_LPR != 64  // (A/B builds) M >= 2: fewer lanes per row, the same rows per workgroup
+            if constexpr (MT >= 2)
+                return gemv_launch<F, MT, 2, QG_GEMVM_LPR, gemvm_wgs<F> * QG_GEMVM_LPR / 64, SUMI, AIN, false, true>(g, st);
+#endif
             return gemv_launch<F, MT, 2, 64, MT == 1 ? gemv1l_wgs<F> : gemvm_wgs<F>, SUMI, AIN, false, true>(g, st);
         }
     }

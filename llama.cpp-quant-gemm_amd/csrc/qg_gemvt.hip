@@ -35,12 +35,6 @@ namespace {
 #ifndef QG_GEMVT_NU
 #define QG_GEMVT_NU 0  // 0: per K (gemvt_nu below)
 #endif
-#ifndef QG_GEMVT_RED
-#define QG_GEMVT_RED 0  // cross-wave sum: 0 after a workgroup barrier (wave 0 sums), 1 by the last wave to finish
-#endif
-#ifndef QG_GEMVT_ABL
-#define QG_GEMVT_ABL 0  // (A/B ablation builds only) 1: no cross-wave sum, 2: no staging, 4: no dot
-#endif
 
 constexpr int GT_SB = 4;  // blocks per stage (tiled_fmt)
 
@@ -69,22 +63,24 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
     // 1) the lane's first activation block (staging item 0), then every weight unit of the lane
     const int RSTR = 48 * MT + 4;  // record dwords per staged stage (12 per block and token, +4: bank spread)
     uint32_t* wl = lds + wave * (NU * SL) * RSTR;
-    uint32_t ab[9];
-    auto load_ablk = [&](int it) {  // staging item it = m * NBW + jb
+    constexpr int NIT = (NBW * MT + 63) / 64;  // staging items per lane, ALL loaded before the weight stream
+    uint32_t ab[NIT][9];
+    auto load_ablk = [&](int it, uint32_t (&d)[9]) {  // staging item it = m * NBW + jb
         const int m = it / NBW, jb = it % NBW, gb = wave * NBW + jb;
         if (m >= M || gb >= (TA ? H * GT_SB : nb)) {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) ab[i] = 0u;
+            for (int i = 0; i < 9; ++i) d[i] = 0u;
             return;
         }
         long src = ((long)m * nb + gb) * 9;
         if constexpr (TA)  // block gb of token m inside its tile's 2304-B stage run (zero padding blocks)
             src = (((long)(m / ACT_TILE) * H + (gb >> 2)) * ACT_TILE + m % ACT_TILE) * 36 + (gb & 3) * 9;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) ab[i] = A[src + i];
+        for (int i = 0; i < 9; ++i) d[i] = A[src + i];
     };
-    constexpr int NIT = (NBW * MT + 63) / 64;  // staging items per lane
-    if (!(QG_GEMVT_ABL & 2)) load_ablk(lane);
+#pragma unroll
+    for (int k = 0; k < NIT; ++k)
+        if (lane + 64 * k < NBW * MT) load_ablk(lane + 64 * k, ab[k]);
 
     uint32_t wu[NU][UDW];
 #pragma unroll
@@ -113,22 +109,13 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
         }
     }
 
-    if (QG_GEMVT_RED == 1 && !SUMI) {
-        // the last-arriver counter of the cross-wave sum: zeroed, then one barrier while the loads are in
-        // flight (LDS writes drained, no wait on the global loads)
-        if (threadIdx.x == 0) lds[W * (NU * SL) * RSTR + MT * W * R] = 0u;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-
     // 2) the wave's records: item it -> stage-local block jb = 4 jl + b, token m, at jl * RSTR + (b MT + m) * 12
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
         const int it = lane + 64 * k;
-        if (QG_GEMVT_ABL & 2) break;
         if (it < NBW * MT) {
-            if (k) load_ablk(it);
             const int m = it / NBW, jb = it % NBW;
-            make_act_record<F>(ab, wl + (jb >> 2) * RSTR + ((jb & 3) * MT + m) * 12);
+            make_act_record<F>(ab[k], wl + (jb >> 2) * RSTR + ((jb & 3) * MT + m) * 12);
         }
     }
     // the records were written by other lanes of this wave: LDS executes a wave's instructions in order, so
@@ -184,7 +171,7 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m] = group_sum_last<SL>(acc[m]);
         const bool last = s == SL - 1;
-        if (W == 1 || (QG_GEMVT_ABL & 1)) {
+        if (W == 1) {
             if (last && n < N) {
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
@@ -197,24 +184,6 @@ __global__ __launch_bounds__(1024) void gemvt_kernel(const uint32_t* __restrict_
         if (last) {
 #pragma unroll
             for (int m = 0; m < MT; ++m) red[(m * W + wave) * R + r] = acc[m];
-        }
-        if (QG_GEMVT_RED == 1) {
-            // the last wave to arrive sums: a wave's LDS operations execute in order, so when its counter
-            // add returns W - 1 every other wave's partials are in LDS (no workgroup barrier)
-            uint32_t* cnt = reinterpret_cast<uint32_t*>(red + MT * W * R);
-            uint32_t prev = 0;
-            if (lane == 0) prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            prev = __builtin_amdgcn_readfirstlane(prev);
-            if (prev != (uint32_t)(W - 1)) return;
-            if (lane < R * MT) {
-                const int m = lane / R, rw = lane % R, nn = tile * R + rw;
-                if (m < M && nn < N) {
-                    float v = red[m * W * R + rw];
-                    for (int w = 1; w < W; ++w) v += red[(m * W + w) * R + rw];
-                    static_cast<float*>(out)[(long)m * ldc_m + (long)nn * ldc_n] = v;
-                }
-            }
-            return;
         }
         __syncthreads();
         const int tid = threadIdx.x;
@@ -246,7 +215,7 @@ template <int F, int MT, int R, int NU> hipError_t gemvt_launch(const GemmArgs& 
     const int nb = g.K / QK, H = (nb + GT_SB - 1) / GT_SB;
     const int W = (H + NU * SL - 1) / (NU * SL);
     const int grid = (g.N + R - 1) / R;
-    const size_t lds = ((size_t)W * NU * SL * (48 * MT + 4) + (size_t)W * R * MT + 4) * 4;
+    const size_t lds = ((size_t)W * NU * SL * (48 * MT + 4) + (size_t)W * R * MT) * 4;
     const bool ta = g.lay == LAY_TILED_ACT;
     if (g.describe) {
         describe_kernel(g, "gemvt F=%d MT=%d R=%d NU=%d W=%d TA=%d grid=%d", F, MT, R, NU, W, (int)ta, grid);
