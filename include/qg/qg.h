@@ -134,13 +134,22 @@ int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, i
  * restated in oracle/oracle.py (tile_weights); one streaming kernel.
  * qg_gemm_w4a8_tiled then computes the same product as qg_gemm_w4a8(A, B, ...) (activation-major,
  * A: block_q8_1 [M][K/32], 16-B aligned; within the reassociation bound of the MFMA kernel, DESIGN.md
- * §5; at M = 1 the tiled decode GEMV, whose per-block terms are the reference's bit for bit) from B_tiled
- * in ONE launch for every M — the prefill's weight stages are one linear stream instead of 32 row
- * segments (decode-heavy callers: the reference rows' GEMV stays faster at M = 1). K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
+ * §5; for M <= 4 the tiled decode GEMV, whose per-block terms are the reference's bit for bit, summed in
+ * a fixed order) from B_tiled in ONE launch for every M — the prefill's weight stages are one linear
+ * stream instead of 32 row segments. K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
  * activation rows). _ldc: output row stride (>= N floats). qg_debug_sumi_tiled / qg_debug_config_tiled
  * are the parity hook and the configuration query of the same instantiation (as qg_debug_sumi /
  * qg_debug_config below). Replaces the tiled-GEMM role of include/gemm_cuda_tiled.cuh:293-300 and the
- * cp.async-staged kernels/gemm/gemm_async_copy.cuh:65-232 for reused weights. */
+ * cp.async-staged kernels/gemm/gemm_async_copy.cuh:65-232 for reused weights.
+ * DECODE ON THE TILED LAYOUT (measured, one MI355X, Q4_0, N = 4096, profiles/r06_tuning/r6i_ab_tiled_final.txt):
+ * at K = 14336 (the reference's published decode shapes) M = 1 / 2 / 4 run 7.78 / 8.64 / 11.19 us against
+ * 7.62 / 8.76 / 11.17 on the reference rows — one tiled copy serves decode and prefill at no cost; at
+ * N = K = 4096 they run 3.86 / 4.17 / 5.18 us against 3.32 / 3.75 / 4.47 (+11..16 %): a decode-bound caller
+ * at such K keeps the rows for M <= 4 (qg_gemm_w4a8) and tiles a second copy only if its prefill needs it.
+ * Limits (QG_ERR_UNSUPPORTED, nothing launched; the tiled layout has no generic kernel): output strides
+ * past INT32_MAX; M <= 4 with K > 16384 whose shape the MFMA kernel rejects too; tiled weights of a
+ * (tile, stage) run count past 2^31 bytes; plain activation rows of 2 GiB or more under the windowed
+ * (odd K/32) MFMA path. */
 size_t qg_tile_weights_bytes(int N, int K, int wtype);
 int qg_tile_weights(const void* B, void* B_tiled, int N, int K, int wtype, qg_stream_t stream);
 int qg_gemm_w4a8_tiled(const void* A_q8_1, const void* B_tiled, float* C, int M, int N, int K, int wtype,

@@ -112,6 +112,16 @@ def _check_blocks(t: torch.Tensor, what: str, rows: int, K: int, bb: int) -> Non
     _require(t.numel() == expect, f"{what} shape mismatch: expected {expect} elements, got {t.numel()}")
 
 
+def _check_layout(t: torch.Tensor, what: str, nbytes: int, device) -> None:
+    """A load-time layout buffer (tiled / packed weights, tiled activations) handed to the C-ABI as a raw
+    pointer: the exact byte count, uint8, contiguous, on the product's device (a strided view
+    or a non-uint8 tensor of matching numel would otherwise be read as the wrong bytes)."""
+    _require(t.dtype == torch.uint8, f"{what} must be a uint8 tensor, got {t.dtype}")
+    _require(t.is_contiguous(), f"{what} must be contiguous")
+    _require(t.is_cuda and t.device == device, f"{what} must be on {device}, got {t.device}")
+    _require(t.numel() == nbytes, f"{what} shape mismatch: expected {nbytes} bytes, got {t.numel()}")
+
+
 def gemm_w4a8(activation_q: torch.Tensor, weight_q: torch.Tensor, M: int, N: int, K: int,
               wtype: int = Q4_0, algo: int = ALGO_AUTO, out: torch.Tensor | None = None) -> torch.Tensor:
     """Activation-major C[M, N] = A_q8_1[M, K] . B_w[N, K]^T (include/gemm_reference.h:175-222;
@@ -222,11 +232,10 @@ def gemm_w4a8_prepacked(activation_q: torch.Tensor, weight_packed: torch.Tensor,
                         wtype: int = Q4_0) -> torch.Tensor:
     """C [M, N] = the same product as gemm_w4a8(activation_q, weight_q, ...) from
     repack_weights(weight_q) (qg_gemm_w4a8_prepacked; K is the logical K)."""
-    _require(activation_q.is_cuda and weight_packed.is_cuda, "Inputs must be CUDA tensors")
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
-    _require(activation_q.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    _check_blocks(activation_q, "Activation", M, K, 36)
     lib = _lib.load()
-    _require(weight_packed.numel() == lib.qg_repack_weights_bytes(N, K, wtype), "Packed weight shape mismatch")
+    _check_layout(weight_packed, "weight_packed", lib.qg_repack_weights_bytes(N, K, wtype), activation_q.device)
     a = activation_q.contiguous()
     out = torch.empty((M, N), dtype=torch.float32, device=a.device)
     wsb = lib.qg_gemm_w4a8_prepacked_workspace_size(M, K)
@@ -256,11 +265,10 @@ def gemm_w4a8_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: i
                     wtype: int = Q4_0, out: torch.Tensor | None = None) -> torch.Tensor:
     """C [M, N] = the same product as gemm_w4a8(activation_q, weight_q, ...) from
     tile_weights(weight_q) (qg_gemm_w4a8_tiled; any K % 32 == 0)."""
-    _require(activation_q.is_cuda and weight_tiled.is_cuda, "Inputs must be CUDA tensors")
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
-    _require(activation_q.numel() == M * (K // 32) * 36, "Activation shape mismatch")
+    _check_blocks(activation_q, "Activation", M, K, 36)
     lib = _lib.load()
-    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    _check_layout(weight_tiled, "weight_tiled", lib.qg_tile_weights_bytes(N, K, wtype), activation_q.device)
     a = activation_q.contiguous()
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=a.device)
@@ -304,11 +312,11 @@ def gemm_w4a8_tiled_act(activation_tiled: torch.Tensor, weight_tiled: torch.Tens
                         wtype: int = Q4_0, out: torch.Tensor | None = None) -> torch.Tensor:
     """C [M, N] = gemm_w4a8_tiled's product with the activations in the tiled layout too
     (qg_gemm_w4a8_tiled_act)."""
-    _require(activation_tiled.is_cuda and weight_tiled.is_cuda, "Inputs must be CUDA tensors")
     _require(K % 32 == 0, f"K must be divisible by 32, got {K}")
     lib = _lib.load()
-    _require(activation_tiled.numel() == lib.qg_activations_tiled_bytes(M, K), "Tiled activation shape mismatch")
-    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    _require(weight_tiled.is_cuda, "weight_tiled must be a CUDA tensor")
+    _check_layout(activation_tiled, "activation_tiled", lib.qg_activations_tiled_bytes(M, K), weight_tiled.device)
+    _check_layout(weight_tiled, "weight_tiled", lib.qg_tile_weights_bytes(N, K, wtype), weight_tiled.device)
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=weight_tiled.device)
     _require(out.is_cuda and out.dtype == torch.float32 and out.shape == (M, N) and out.is_contiguous(),
@@ -338,10 +346,10 @@ def gemm_w4a8_padded(activation_padded: torch.Tensor, weight_packed: torch.Tenso
                      wtype: int = Q4_0) -> torch.Tensor:
     """C [M, N] from quantize_q8_1_padded activations and repack_weights weights, one launch
     (qg_gemm_w4a8_padded; K is the logical K)."""
-    _require(activation_padded.is_cuda and weight_packed.is_cuda, "Inputs must be CUDA tensors")
+    _require(weight_packed.is_cuda, "weight_packed must be a CUDA tensor")
     nbp = (K // 32 + 7) // 8 * 8
-    _require(activation_padded.numel() == M * nbp * 36, "Activation shape mismatch")
-    _require(weight_packed.numel() == N * nbp * BLOCK_BYTES[wtype], "Packed weight shape mismatch")
+    _check_layout(activation_padded.contiguous(), "activation_padded", M * nbp * 36, weight_packed.device)
+    _check_layout(weight_packed, "weight_packed", N * nbp * BLOCK_BYTES[wtype], weight_packed.device)
     out = torch.empty((M, N), dtype=torch.float32, device=weight_packed.device)
     with torch.cuda.device(weight_packed.device):
         _lib.check(_lib.load().qg_gemm_w4a8_padded(_ptr(activation_padded.contiguous()), _ptr(weight_packed), _ptr(out),
@@ -513,7 +521,7 @@ def debug_sumi_tiled(activation_q: torch.Tensor, weight_tiled: torch.Tensor, M: 
     """Per-block int32 dots [M, N, K/32] from the instantiation gemm_w4a8_tiled launches."""
     _check_blocks(activation_q, "Activation", M, K, 36)
     lib = _lib.load()
-    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    _check_layout(weight_tiled, "weight_tiled", lib.qg_tile_weights_bytes(N, K, wtype), activation_q.device)
     out = torch.empty((M, N, K // 32), dtype=torch.int32, device=weight_tiled.device)
     with torch.cuda.device(weight_tiled.device):
         _lib.check(lib.qg_debug_sumi_tiled(_ptr(activation_q.contiguous()), _ptr(weight_tiled), _ptr(out), M, N, K, wtype,
@@ -525,8 +533,9 @@ def debug_sumi_tiled_act(activation_tiled: torch.Tensor, weight_tiled: torch.Ten
                          wtype: int = Q4_0) -> torch.Tensor:
     """Per-block int32 dots [M, N, K/32] from the instantiation gemm_w4a8_tiled_act launches."""
     lib = _lib.load()
-    _require(activation_tiled.numel() == lib.qg_activations_tiled_bytes(M, K), "Tiled activation shape mismatch")
-    _require(weight_tiled.numel() == lib.qg_tile_weights_bytes(N, K, wtype), "Tiled weight shape mismatch")
+    _require(weight_tiled.is_cuda, "weight_tiled must be a CUDA tensor")
+    _check_layout(activation_tiled, "activation_tiled", lib.qg_activations_tiled_bytes(M, K), weight_tiled.device)
+    _check_layout(weight_tiled, "weight_tiled", lib.qg_tile_weights_bytes(N, K, wtype), weight_tiled.device)
     out = torch.empty((M, N, K // 32), dtype=torch.int32, device=weight_tiled.device)
     with torch.cuda.device(weight_tiled.device):
         _lib.check(lib.qg_debug_sumi_tiled_act(_ptr(activation_tiled), _ptr(weight_tiled), _ptr(out), M, N, K, wtype,

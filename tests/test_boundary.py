@@ -208,3 +208,23 @@ def test_ldc_entry_validates(lib):
     # ldc below N is an invalid argument, reported before anything is enqueued
     assert so.qg_gemm_w4a8_ldc(P(256), P(256), P(256), 2, 64, 256, 32, 2, 0, None) == -1
     assert so.qg_gemm_w4a8_ldc(P(256), P(256), P(256), 2, 64, 100, 64, 2, 0, None) == -2
+
+
+def test_layout_buffers_checked_before_launch():
+    """the tiled / packed layout buffers the Python face hands to the C-ABI as raw pointers are
+    checked for dtype, contiguity, device and exact size first (CPU tensors: refused before any launch)."""
+    import pytest
+    import torch
+    import quant_gemm as qg
+    a = torch.zeros(2 * 4 * 36, dtype=torch.uint8)
+    w = torch.zeros(64, dtype=torch.uint8)
+    for fn, args in [(qg.gemm_w4a8_tiled, (a, w, 2, 32, 128)), (qg.debug_sumi_tiled, (a, w, 2, 32, 128)),
+                     (qg.gemm_w4a8_tiled_act, (w, w, 2, 32, 128)), (qg.debug_sumi_tiled_act, (w, w, 2, 32, 128)),
+                     (qg.gemm_w4a8_prepacked, (a, w, 2, 32, 128))]:
+        with pytest.raises(RuntimeError):
+            fn(*args)
+    # a float tensor of the right byte count / a strided view: refused by the layout check itself
+    with pytest.raises(RuntimeError, match="uint8"):
+        qg._check_layout(torch.zeros(16, dtype=torch.float32), "weight_tiled", 16, torch.device("cpu"))
+    with pytest.raises(RuntimeError, match="contiguous"):
+        qg._check_layout(torch.zeros(32, dtype=torch.uint8)[::2], "weight_tiled", 16, torch.device("cpu"))
