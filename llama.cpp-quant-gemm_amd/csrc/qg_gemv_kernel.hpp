@@ -288,6 +288,13 @@ typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // tile's weight unit is in flight before the staging barrier. Each row's arithmetic is unchanged, so
 // outputs are bit-identical to TPW = 1 (used by the batched and grouped launches, whose grids have
 // thousands of workgroups; the single launch keeps one tile per workgroup to fill the CUs).
+// The largest M tile whose unit loop preloads the unit's records (0: per format — 4 for the byte-decode formats
+// on their 512-thread workgroups, 2 for the nibble-plane ones: profiles/r06_tuning/r6l_ab_gemv_pre_mt4.txt, M = 4,
+// K = 14336: Q5_0 19.18 -> 18.64 us, Q8_0 19.02 -> 18.27, but Q4_0 11.21 -> 12.32, Q4_1 12.00 -> 16.23)
+#ifndef QG_GEMV_PRE_MT
+#define QG_GEMV_PRE_MT 0
+#endif
+template <int F> constexpr int gemv_pre_mt = QG_GEMV_PRE_MT ? QG_GEMV_PRE_MT : (F == FMT_Q4_0 || F == FMT_Q4_1) ? 2 : 4;
 #ifndef QG_GEMV_ACT2
 #define QG_GEMV_ACT2 1  // (A/B builds) 0: M >= 2 loads each further activation block after the previous record
 #endif
@@ -631,7 +638,8 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     if (g.group && (SUMI || AIN != AIN_Q8_1 || NT || MT > 4)) return hipErrorInvalidValue;  // no grouped form here
     if (g.describe) {  // qg_debug_config: name the instantiation instead of launching it
         describe_kernel(g, "gemv F=%d MT=%d BPL=%d LPR=%d WGS=%d AIN=%d NT=%d PRE=%d ONEU=%d SIG=%s grid=%dx%d", F, MT, BPL,
-                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= 2)), oneu, m1 ? "m1" : shrt ? "short" : "full",
+                        LPR, WGS, AIN, (int)NT, (int)(one ? PRE : (PRE && MT <= (shrt && !oneu ? gemv_pre_mt<F> : 2))), oneu,
+                        m1 ? "m1" : shrt ? "short" : "full",
                         grid, g.batch);
         return hipSuccess;
     }
@@ -696,7 +704,7 @@ hipError_t gemv_launch(const GemmArgs& g, hipStream_t st) {
     // one product with 32-bit output strides: the short-argument entry (gemvs_kernel)
     if (shrt) {
         auto ks = one ? gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE, 1>
-                      : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 0>;
+                      : gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= gemv_pre_mt<F>), 0>;
         if constexpr (NU_OK && MT > 1) {
             if (nu == 2) ks = gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 2>;
             if (nu == 4) ks = gemvs_kernel<F, MT, BPL, LPR, WGS, SUMI, AIN, PRE && (MT <= 2), 4>;
