@@ -225,7 +225,8 @@ int run_gemm(GemmArgs& g, int algo, hipStream_t st) {
     return QG_OK;
 }
 
-// The tiled weight layout (qg_tile_weights): the tiled decode GEMV for M <= 4 (qg_gemvt.hip, round 6), the
+// The tiled weight layout (qg_tile_weights): the MFMA small-batch decode for M = 3..4 and M = 2 at K/32 > 256
+// (qg_gemvm.hip), the tiled decode GEMV for the rest of M <= 4 (qg_gemvt.hip, round 6), the
 // MFMA kernels beyond (LAY_TILED; odd K/32 through its activation windows). Shapes neither
 // takes (ldc past INT32_MAX, activation windows of 2 GiB or more, K/32 whose records exceed the LDS at
 // M <= 4 where the MFMA kernel rejects the shape too) return QG_ERR_UNSUPPORTED: the tiled layout has no
@@ -237,6 +238,10 @@ int run_tiled(GemmArgs& g, hipStream_t st) {
     if (g.M == 0 || g.N == 0) return QG_OK;
     if (!g.A || !g.B || (!g.C && !g.sumi)) return QG_ERR_INVALID_ARG;
     if (((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 15) != 0) return QG_ERR_ALIGN;
+#ifndef QG_TILED_GEMVM  // (A/B builds: 0 = the round-6 tiled decode GEMV for every M <= 4)
+#define QG_TILED_GEMVM 1
+#endif
+    if (QG_TILED_GEMVM && gemvm_eligible(g)) return hip_status(launch_gemvm(g, st));  // M = 3..4 (2 at long K)
     if (gemvt_eligible(g)) return hip_status(launch_gemvt(g, st));  // M <= 4: the tiled decode GEMV
     if (!mfma_eligible(g)) return QG_ERR_UNSUPPORTED;
     return hip_status(launch_mfma(g, st));

@@ -90,6 +90,11 @@ hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
 bool gemvt_eligible(const GemmArgs& g);
 hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st);
 
+// Small-batch decode (M = 3..4, and 2 at K/32 > 256) on the tiled layout (qg_gemvm.hip, round 6): 16-row half tiles, the QS
+// pieces straight from HBM into v_mfma_i32_16x16x32_i8 operands, the prefill's MFMA-assisted epilogue.
+bool gemvm_eligible(const GemmArgs& g);
+hipError_t launch_gemvm(const GemmArgs& g, hipStream_t st);
+
 // Prefill (M >= 5): LDS-DMA staged weights + activations, one v_mfma_i32_16x16x32_i8 per Q-block,
 // MFMA-assisted (v_mfma_f32_16x16x16_f16) scale epilogue.
 bool mfma_eligible(const GemmArgs& g);

@@ -71,7 +71,7 @@ def instructions(listing):
 
 
 def test_mfma_results_padded(listing):
-    checked, violations, mfmas, wide = 0, [], 0, []
+    checked, violations, mfmas, wide, chained = 0, [], 0, [], 0
     for fn, body in instructions(listing):
         for i, ins in enumerate(body):
             if not ins.startswith("v_mfma"):
@@ -93,6 +93,7 @@ def test_mfma_results_padded(listing):
                         # matrix pipe's own interlock and hipcc's; once another MFMA rewrites these
                         # registers, later readers belong to it (checked from its own position)
                         if regs(nxt.split(None, 1)[1].split(",")[0]) & dst:
+                            chained += 1
                             break
                     else:
                         checked += 1
@@ -104,5 +105,41 @@ def test_mfma_results_padded(listing):
                 states += int(m.group(1)) + 1 if m else 1
     assert mfmas > 100, "expected the prefill / W4A16 MFMA kernels in the library"
     assert any("_32x32x" in f for f in wide), "expected the large-M prefill's 32 x 32 MFMAs"
-    assert checked > mfmas // 4, (checked, mfmas)
+    # (accumulation chains: only the last MFMA of a chain has its result read by another unit)
+    assert checked > (mfmas - chained) // 4, (checked, mfmas, chained)
+    assert not violations, "\n".join(violations[:20])
+
+
+# Cross-opcode MFMA register reuse (round 6, qg_gemvm.hip header): an MFMA that writes registers which an
+# MFMA of ANOTHER opcode issued shortly before still reads as its accumulator input (into a different
+# destination) or writes itself. hipcc emitted `i8 v[22:25] <- C bias; i8 v[14:17] <- C v[22:25]; f16
+# v[22:25]` with 0 wait states, and on an MI355X the f16 result came out wrong whenever CUs held several
+# workgroups. In-place accumulation (vdst == SrcC, the next MFMA reading the same registers) is the matrix
+# pipe's own chain and is allowed.
+MFMA_REUSE_STATES = 16
+
+
+def test_no_cross_opcode_mfma_register_reuse(listing):
+    violations, mfmas = [], 0
+    for fn, body in instructions(listing):
+        for i, ins in enumerate(body):
+            if not ins.startswith("v_mfma"):
+                continue
+            mfmas += 1
+            op1 = ins.split()[0]
+            ops = [o.strip() for o in ins.split(None, 1)[1].split(",")]
+            dst = regs(ops[0])
+            srcc = regs(ops[3]) if len(ops) > 3 else set()
+            states = 0
+            for nxt in body[i + 1:]:
+                op = nxt.split()[0]
+                if op.startswith(STOP) or states >= MFMA_REUSE_STATES:
+                    break
+                if op.startswith("v_mfma") and op != op1:
+                    d2 = regs(nxt.split(None, 1)[1].split(",")[0])
+                    if d2 & (srcc - dst) or d2 & dst:
+                        violations.append(f"{fn}: {ins} -> {nxt} after {states} wait states")
+                m = re.match(r"s_nop\s+(\d+)", nxt)
+                states += int(m.group(1)) + 1 if m else 1
+    assert mfmas > 100
     assert not violations, "\n".join(violations[:20])
