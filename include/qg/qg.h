@@ -134,18 +134,20 @@ int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, i
  * restated in oracle/oracle.py (tile_weights); one streaming kernel.
  * qg_gemm_w4a8_tiled then computes the same product as qg_gemm_w4a8(A, B, ...) (activation-major,
  * A: block_q8_1 [M][K/32], 16-B aligned; within the reassociation bound of the MFMA kernel, DESIGN.md
- * §5; for M <= 4 the tiled decode GEMV, whose per-block terms are the reference's bit for bit, summed in
- * a fixed order) from B_tiled in ONE launch for every M — the prefill's weight stages are one linear
+ * §5; for M = 1..2 the tiled decode GEMV, whose per-block terms are the reference's bit for bit, summed in
+ * a fixed order; for M = 3..4, and M = 2 at K/32 > 256, the MFMA small-batch decode, within the same
+ * reassociation bound) from B_tiled in ONE launch for every M — the prefill's weight stages are one linear
  * stream instead of 32 row segments. K/32 need not be a multiple of 4 or 8 (the kernel windows the plain
  * activation rows). _ldc: output row stride (>= N floats). qg_debug_sumi_tiled / qg_debug_config_tiled
  * are the parity hook and the configuration query of the same instantiation (as qg_debug_sumi /
  * qg_debug_config below). Replaces the tiled-GEMM role of include/gemm_cuda_tiled.cuh:293-300 and the
  * cp.async-staged kernels/gemm/gemm_async_copy.cuh:65-232 for reused weights.
- * DECODE ON THE TILED LAYOUT (measured, one MI355X, Q4_0, N = 4096, profiles/r06_tuning/r6i_ab_tiled_final.txt):
- * at K = 14336 (the reference's published decode shapes) M = 1 / 2 / 4 run 7.78 / 8.64 / 11.19 us against
- * 7.62 / 8.76 / 11.17 on the reference rows — one tiled copy serves decode and prefill at no cost; at
- * N = K = 4096 they run 3.86 / 4.17 / 5.18 us against 3.32 / 3.75 / 4.47 (+11..16 %): a decode-bound caller
- * at such K keeps the rows for M <= 4 (qg_gemm_w4a8) and tiles a second copy only if its prefill needs it.
+ * DECODE ON THE TILED LAYOUT (measured, one MI355X, N = 4096, profiles/r06_tuning/r6o_ab_tiled_decode_final.txt):
+ * at K = 14336 (the reference's published decode shapes) Q4_0 M = 1 / 2 / 3 / 4 / 8 run 7.77 / 8.27 / 9.10 /
+ * 9.39 / 9.82 us against 7.65 / 8.84 / 10.45 / 11.31 / 10.11 on the reference rows (Q8_0 M = 4 13.49 vs 18.32)
+ * — one tiled copy serves decode and prefill; at N = K = 4096 M = 1 / 2 / 3 / 4 run 3.94 / 4.18 / 4.51 / 4.53
+ * against 3.39 / 3.75 / 4.15 / 4.49: a caller bound by single-token decode at such K keeps the rows for M <= 2
+ * (qg_gemm_w4a8) and tiles a second copy only if its batched decode or prefill needs it.
  * Limits (QG_ERR_UNSUPPORTED, nothing launched; the tiled layout has no generic kernel): output strides
  * past INT32_MAX; M <= 4 with K > 16384 whose shape the MFMA kernel rejects too; tiled weights of a
  * (tile, stage) run count past 2^31 bytes; plain activation rows of 2 GiB or more under the windowed

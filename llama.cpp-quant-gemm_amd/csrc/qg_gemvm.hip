@@ -259,8 +259,8 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
     }
 }
 
-// Token columns (M rounded up to a power of two) and stages per lane: the fewest in {2, 4, 8} with at most
-// 16 waves (K <= 65536)
+// Token columns (M rounded up to a power of two) and stages per lane: the fewest in {2, 4, 8} (at most 16
+// waves: K <= 16384, as the tiled decode GEMV)
 inline int gemvm_mp(int M) { return M <= 2 ? 2 : 4; }
 inline int gemvm_nu(int, int H) { return H <= 32 ? 2 : H <= 64 ? 4 : 8; }
 inline size_t gemvm_lds(int M, int H) {
