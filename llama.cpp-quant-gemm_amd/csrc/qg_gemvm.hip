@@ -63,8 +63,8 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
     constexpr int NIT = (NBW * MP + 63) / 64; // staged activation blocks per lane
     static_assert(NBW % BPC == 0 && SPAN <= 16, "groups of whole blocks, scale operand of <= 4 stages");
     // register ring of weight stages: all NU of them under the 128-VGPR cap of 1024-thread workgroups, but 4
-    // for Q5_1 at NU = 8 (its 48-B stage pieces: scratch otherwise)
-    constexpr int RS = F == FMT_Q5_1 && NU > 4 ? 4 : NU;
+    // at NU = 8 for Q5_x (their qh pieces) and for 8 token columns (36 staged dwords): scratch otherwise
+    constexpr int RS = (F == FMT_Q5_0 || F == FMT_Q5_1 || MP == 8) && NU > 4 ? 4 : NU;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
     const int nb = K / QK, H = (nb + MMQ_SB - 1) / MMQ_SB;
@@ -204,8 +204,12 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
                          : GM_OUT
                          : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]), [a2] "v"(af[2]),
                            [b2] "v"(bsel[2]), [a3] "v"(af[3]), [b3] "v"(bsel[3]));
+        } else if constexpr (BPC == 2) {
+            asm volatile(GM_HEAD GM_CC(0) GM_CC(1) GM_TAIL
+                         : GM_OUT
+                         : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]));
         } else {
-            static_assert(BPC == 8, "MP in {2, 4}");
+            static_assert(BPC == 8, "MP in {2, 4, 8}");
             asm volatile(GM_HEAD GM_CC(0) GM_CC(1) GM_CC(2) GM_CC(3) GM_CC(4) GM_CC(5) GM_CC(6) GM_CC(7) GM_TAIL
                          : GM_OUT
                          : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]), [a2] "v"(af[2]),
@@ -261,7 +265,10 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
 
 // Token columns (M rounded up to a power of two) and stages per lane: the fewest in {2, 4, 8} (at most 16
 // waves: K <= 16384, as the tiled decode GEMV)
-inline int gemvm_mp(int M) { return M <= 2 ? 2 : 4; }
+#ifndef QG_GEMVM_MAXM  // (A/B builds: 8 = also M = 5..8 with 8 token columns)
+#define QG_GEMVM_MAXM 4
+#endif
+inline int gemvm_mp(int M) { return M <= 2 ? 2 : M <= 4 ? 4 : 8; }
 inline int gemvm_nu(int, int H) { return H <= 32 ? 2 : H <= 64 ? 4 : 8; }
 inline size_t gemvm_lds(int M, int H) {
     const int NU = gemvm_nu(M, H), W = (H + NU - 1) / NU;
@@ -295,6 +302,9 @@ template <int F, int NU, int MP> hipError_t gemvm_launch(const GemmArgs& g, hipS
 template <int F, int NU> hipError_t gemvm_m(const GemmArgs& g, hipStream_t st) {
     switch (gemvm_mp(g.M)) {
         case 2: return gemvm_launch<F, NU, 2>(g, st);
+#if QG_GEMVM_MAXM > 4
+        case 8: return gemvm_launch<F, NU, 8>(g, st);
+#endif
         default: return gemvm_launch<F, NU, 4>(g, st);
     }
 }
@@ -315,7 +325,7 @@ template <int F> hipError_t gemvm_f(const GemmArgs& g, hipStream_t st) {
 // 8 token columns ran 2x the MFMA kernel's time and stay with it). One product with 32-bit output strides;
 // B_tiled 16-B and A 4-B aligned; the wave records within the LDS; at most 16 waves.
 bool gemvm_eligible(const GemmArgs& g) {
-    if (!(g.lay == LAY_TILED || g.lay == LAY_TILED_ACT) || g.M < 2 || g.M > 4 || g.N < 1 || g.K % QK != 0) return false;
+    if (!(g.lay == LAY_TILED || g.lay == LAY_TILED_ACT) || g.M < 2 || g.M > QG_GEMVM_MAXM || g.N < 1 || g.K % QK != 0) return false;
     if (g.M == 2 && g.K / QK <= 256) return false;
     if (g.batch != 1 || g.group || g.ain != AIN_Q8_1 || ((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 3) != 0) return false;
     if (g.ldc_m > INT32_MAX || g.ldc_n > INT32_MAX || g.ldc_m < 0 || g.ldc_n < 0) return false;

@@ -143,3 +143,32 @@ def test_no_cross_opcode_mfma_register_reuse(listing):
                 states += int(m.group(1)) + 1 if m else 1
     assert mfmas > 100
     assert not violations, "\n".join(violations[:20])
+
+
+def test_hot_kernels_use_no_scratch(tmp_path):
+    """Every hot-path kernel (GEMV, tiled decode GEMV, MFMA small-batch decode, MFMA prefill, large-M prefill)
+    keeps its live values in registers: private_segment_fixed_size 0 in the code object metadata. A spill
+    under the 128-VGPR cap of a 1024-thread workgroup (round 6: the small-batch decode's Q5_0 ring at 8 stages
+    per lane) turns into scratch traffic on every launch."""
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (os.path.exists(OBJDUMP) and os.path.exists(readelf) and os.path.exists(LIB)):
+        pytest.skip("llvm tools or libqg_hip.so missing")
+    so = shutil.copy(LIB, tmp_path / "libqg_hip.so")
+    subprocess.run([OBJDUMP, "--offloading", str(so)], cwd=tmp_path, capture_output=True, check=True)
+    notes = ""
+    for f in sorted(os.listdir(tmp_path)):
+        if "gfx950" in f:
+            notes += subprocess.run([readelf, "--notes", str(tmp_path / f)], capture_output=True, text=True,
+                                    check=True).stdout
+    sizes, name = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s*\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+        if m and name:
+            sizes[name] = int(m.group(1))
+    hot = {n: v for n, v in sizes.items() if re.search(r"(gemv|gemvt|gemvm|mmq|mmqt|mmql)\w*_kernel", n)}
+    assert len(hot) > 100, len(hot)
+    spills = sorted(n for n, v in hot.items() if v)
+    assert not spills, spills[:20]
