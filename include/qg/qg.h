@@ -145,8 +145,8 @@ int qg_gemm_w4a8_prepacked(const void* A_q8_1, const void* B_packed, float* C, i
  * DECODE ON THE TILED LAYOUT (measured, one MI355X, N = 4096, profiles/r06_tuning/r6o_ab_tiled_decode_final.txt):
  * at K = 14336 (the reference's published decode shapes) Q4_0 M = 1 / 2 / 3 / 4 / 8 run 7.77 / 8.27 / 9.10 /
  * 9.39 / 9.82 us against 7.65 / 8.84 / 10.45 / 11.31 / 10.11 on the reference rows (Q8_0 M = 4 13.49 vs 18.32)
- * — one tiled copy serves decode and prefill; at N = K = 4096 M = 1 / 2 / 3 / 4 run 3.94 / 4.18 / 4.51 / 4.53
- * against 3.39 / 3.75 / 4.15 / 4.49: a caller bound by single-token decode at such K keeps the rows for M <= 2
+ * — one tiled copy serves decode and prefill; at N = K = 4096 M = 1 / 2 / 3 / 4 run 3.94 / 4.18 / 4.30 / 4.38
+ * against 3.39 / 3.75 / 4.21 / 4.50: a caller bound by single-token decode at such K keeps the rows for M <= 2
  * (qg_gemm_w4a8) and tiles a second copy only if its batched decode or prefill needs it.
  * Limits (QG_ERR_UNSUPPORTED, nothing launched; the tiled layout has no generic kernel): output strides
  * past INT32_MAX; M <= 4 with K > 16384 whose shape the MFMA kernel rejects too; tiled weights of a

@@ -263,13 +263,22 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
     }
 }
 
-// Token columns (M rounded up to a power of two) and stages per lane: the fewest in {2, 4, 8} (at most 16
-// waves: K <= 16384, as the tiled decode GEMV)
+// Token columns (M rounded up to a power of two) and stages per lane: 4 up to K/32 = 256, then 8 (at most 16
+// waves: K <= 16384, as the tiled decode GEMV). 4 rather than 2 stages per lane at K/32 <= 128
+// (profiles/r06_tuning/r6q_ab_gemvm_nu_m2.txt): M = 4 N = K = 4096 4.53 -> 4.38 us, M = 3 4.50 -> 4.30, M = 4
+// N = 11008 8.20 -> 7.03; M = 2 stays with the tiled decode GEMV up to K/32 = 256 either way (4.14 vs 4.45 at
+// K = 4096, 6.03 vs 5.99 at 8192).
 #ifndef QG_GEMVM_MAXM  // (A/B builds: 8 = also M = 5..8 with 8 token columns)
 #define QG_GEMVM_MAXM 4
 #endif
 inline int gemvm_mp(int M) { return M <= 2 ? 2 : M <= 4 ? 4 : 8; }
-inline int gemvm_nu(int, int H) { return H <= 32 ? 2 : H <= 64 ? 4 : 8; }
+#ifndef QG_GEMVM_NU_SMALL  // (A/B builds: stages per lane up to K/32 = 128)
+#define QG_GEMVM_NU_SMALL 4
+#endif
+#ifndef QG_GEMVM_M2_MIN_NB  // (A/B builds: M = 2 from this K/32 on)
+#define QG_GEMVM_M2_MIN_NB 257
+#endif
+inline int gemvm_nu(int, int H) { return H <= 32 ? QG_GEMVM_NU_SMALL : H <= 64 ? 4 : 8; }
 inline size_t gemvm_lds(int M, int H) {
     const int NU = gemvm_nu(M, H), W = (H + NU - 1) / NU;
     return ((size_t)W * NU * MMQ_SB * gemvm_mp(M) * 9 + (size_t)W * 256) * 4;
@@ -326,7 +335,7 @@ template <int F> hipError_t gemvm_f(const GemmArgs& g, hipStream_t st) {
 // B_tiled 16-B and A 4-B aligned; the wave records within the LDS; at most 16 waves.
 bool gemvm_eligible(const GemmArgs& g) {
     if (!(g.lay == LAY_TILED || g.lay == LAY_TILED_ACT) || g.M < 2 || g.M > QG_GEMVM_MAXM || g.N < 1 || g.K % QK != 0) return false;
-    if (g.M == 2 && g.K / QK <= 256) return false;
+    if (g.M == 2 && g.K / QK < QG_GEMVM_M2_MIN_NB) return false;
     if (g.batch != 1 || g.group || g.ain != AIN_Q8_1 || ((uintptr_t)g.B & 15) != 0 || ((uintptr_t)g.A & 3) != 0) return false;
     if (g.ldc_m > INT32_MAX || g.ldc_n > INT32_MAX || g.ldc_m < 0 || g.ldc_n < 0) return false;
     if (!(g.wtype == FMT_Q4_0 || g.wtype == FMT_Q4_1 || g.wtype == FMT_Q5_0 || g.wtype == FMT_Q5_1 || g.wtype == FMT_Q8_0))

@@ -4,7 +4,7 @@
   every block's int32 dot equals the reference's inner loop (include/gemm_reference.h:202-212) — bit-exact;
 * the outputs lie within the MFMA epilogue's reassociation bound of the oracle (oracle.reassoc_tol: the
   d_w d_a sumi part and the offset part rounded separately, W partial tiles summed in fixed order);
-* every format, 2 / 4 / 8 stages per lane, one wave (no cross-wave sum), stages past K/32 (zero padding
+* every format, 4 / 8 stages per lane, one wave (no cross-wave sum), stages past K/32 (zero padding
   blocks, and stages past the last real one in the last wave), ragged N, 2..4 tokens, both activation forms
   (Q8_1 rows and the tiled activation layout), grids that put several workgroups on a CU (the padding-record
   bug of the first version showed only there: qg_gemvm.hip header);
@@ -24,9 +24,9 @@ SHAPES = [
     (4, 4096, 14336),  # M = 4: 4 token columns
     (2, 300, 8224),    # M = 2 from K/32 = 257: a padding block, a last wave with stages past H
     (4, 300, 4128),    # K/32 = 129: padding blocks in the last stage, a last wave with stages past H
-    (3, 64, 160),      # one wave (H = 2), stages past K/32, token 3 of 4 columns repeats token 2
+    (3, 64, 160),      # one wave (H = 2 of its 4 stages), stages past K/32, token 3 of 4 columns repeats token 2
     (3, 1000, 6144),   # 4 stages per lane, ragged N (one half tile past it)
-    (4, 32000, 1024),  # many half tiles (linear order), 2 stages per lane, several workgroups per CU
+    (4, 32000, 1024),  # many half tiles (linear order), 2 waves, several workgroups per CU
     (3, 48, 96),       # K/32 = 3 < one stage
 ]
 
