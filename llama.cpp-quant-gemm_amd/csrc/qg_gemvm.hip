@@ -37,14 +37,18 @@
 // zeroed where the records are read. (2) hipcc's builtins let an f16 MFMA take the registers an i8 MFMA
 // issued just before reads as SrcC (`i8 v[22:25] <- C bias; i8 v[14:17] <- C v[22:25]; f16 v[22:25]`, 0
 // wait states); never shown to be wrong by itself, but each group's MFMAs are ONE asm statement all the
-// same: dd first, the accumulations in place (vdst == SrcC), every other destination early-clobber, 16
-// wait states before the VALU reads (1-2 % slower than the builtins; tests/test_isa_hazards.py checks the
-// shipped code object for cross-opcode MFMA register reuse).
+// same: dd first, the first i8 MFMA from the bias, the rest accumulating in place (vdst == SrcC), every
+// destination early-clobber, 10 wait states before the VALU reads (as fast as the builtins;
+// tests/test_isa_hazards.py checks the shipped code object for cross-opcode MFMA register reuse).
 #include "qg_mmq_kernel.hpp"
 
 namespace qg {
 
 namespace {
+
+#ifndef QG_GEMVM_LEAN  // (A/B builds: 0 = the first form — cc copied from the bias, s_nop 1 inside the chain,
+#define QG_GEMVM_LEAN 1  // 16 wait states at the end; 1-4 % slower, profiles/r06_tuning/r6u_ab_gemvm_lean_groups.txt)
+#endif
 
 typedef _Float16 gm_f16x4 __attribute__((ext_vector_type(4)));
 typedef float gm_f32x4 __attribute__((ext_vector_type(4)));
@@ -187,30 +191,42 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
             if ((j + 1) * MMQ_SB <= b0 + BPC && j + RS < NU) load(j + RS, ring[j % RS]);
         __builtin_amdgcn_sched_barrier(0);
         // The group's MFMAs in ONE asm statement (see the header's hazard note): dd first, the BPC i8 MFMAs
-        // accumulating in place (vdst == SrcC), the compensation MFMA in place, 16 wait states before any
-        // VALU reads a result; early-clobber dd and in/out cc / c2 keep every destination off every operand.
+        // accumulating into one tile, the compensation MFMA in place, then the wait states before any VALU
+        // reads a result; early-clobber dd / cc and in/out c2 keep every destination off every operand.
         long bsel[BPC];
 #pragma unroll
         for (int b = 0; b < BPC; ++b) bsel[b] = cb == b ? (long)bq : 0l;
         gm_f32x4 dd;
+#if QG_GEMVM_LEAN
+        // the chain's first MFMA takes the bias as its SrcC (no per-group copy into cc), the in-place
+        // accumulations back to back (the matrix pipe's own SrcC dependency), 10 wait states at the end
+        v4i cc;
+#define GM_CC0 "v_mfma_i32_16x16x32_i8 %[cc], %[a0], %[b0], %[bias]\n\t"
+#define GM_CC(i) "v_mfma_i32_16x16x32_i8 %[cc], %[a" #i "], %[b" #i "], %[cc]\n\t"
+#define GM_TAIL "v_mfma_f32_16x16x16_f16 %[c2], %[ax], %[bs], %[c2]\n\ts_nop 7\n\ts_nop 1"
+#define GM_OUT [dd] "=&v"(dd), [cc] "=&v"(cc), [c2] "+v"(c2)
+#define GM_IN [ad] "v"(ad), [bd] "v"(bd), [ax] "v"(ax), [bs] "v"(bs), [bias] "v"(bias)
+#else
         v4i cc = bias;
 #define GM_CC(i) "v_mfma_i32_16x16x32_i8 %[cc], %[a" #i "], %[b" #i "], %[cc]\n\ts_nop 1\n\t"
-#define GM_HEAD "s_nop 2\n\tv_mfma_f32_16x16x16_f16 %[dd], %[ad], %[bd], 0\n\t"
+#define GM_CC0 GM_CC(0)
 #define GM_TAIL "v_mfma_f32_16x16x16_f16 %[c2], %[ax], %[bs], %[c2]\n\ts_nop 7\n\ts_nop 7"
 #define GM_OUT [dd] "=&v"(dd), [cc] "+v"(cc), [c2] "+v"(c2)
 #define GM_IN [ad] "v"(ad), [bd] "v"(bd), [ax] "v"(ax), [bs] "v"(bs)
+#endif
+#define GM_HEAD "s_nop 2\n\tv_mfma_f32_16x16x16_f16 %[dd], %[ad], %[bd], 0\n\t"
         if constexpr (BPC == 4) {
-            asm volatile(GM_HEAD GM_CC(0) GM_CC(1) GM_CC(2) GM_CC(3) GM_TAIL
+            asm volatile(GM_HEAD GM_CC0 GM_CC(1) GM_CC(2) GM_CC(3) GM_TAIL
                          : GM_OUT
                          : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]), [a2] "v"(af[2]),
                            [b2] "v"(bsel[2]), [a3] "v"(af[3]), [b3] "v"(bsel[3]));
         } else if constexpr (BPC == 2) {
-            asm volatile(GM_HEAD GM_CC(0) GM_CC(1) GM_TAIL
+            asm volatile(GM_HEAD GM_CC0 GM_CC(1) GM_TAIL
                          : GM_OUT
                          : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]));
         } else {
             static_assert(BPC == 8, "MP in {2, 4, 8}");
-            asm volatile(GM_HEAD GM_CC(0) GM_CC(1) GM_CC(2) GM_CC(3) GM_CC(4) GM_CC(5) GM_CC(6) GM_CC(7) GM_TAIL
+            asm volatile(GM_HEAD GM_CC0 GM_CC(1) GM_CC(2) GM_CC(3) GM_CC(4) GM_CC(5) GM_CC(6) GM_CC(7) GM_TAIL
                          : GM_OUT
                          : GM_IN, [a0] "v"(af[0]), [b0] "v"(bsel[0]), [a1] "v"(af[1]), [b1] "v"(bsel[1]), [a2] "v"(af[2]),
                            [b2] "v"(bsel[2]), [a3] "v"(af[3]), [b3] "v"(bsel[3]), [a4] "v"(af[4]), [b4] "v"(bsel[4]),
@@ -218,6 +234,7 @@ __global__ __launch_bounds__(1024) void gemvm_kernel(const uint32_t* __restrict_
                            [b7] "v"(bsel[7]));
         }
 #undef GM_CC
+#undef GM_CC0
 #undef GM_HEAD
 #undef GM_TAIL
 #undef GM_OUT
