@@ -202,6 +202,30 @@ def test_headline_configs_kernels(lib):
     assert qg.debug_config(1, 4000, 4096, 2).startswith("gemv F=2 MT=1 ")
 
 
+def test_tiled_decode_routing():
+    """The tiled entry's decode routing (round 6; CPU: the configuration query launches nothing):
+    M = 1..2 the tiled decode GEMV up to K/32 = 256, M = 3..4 (and M = 2 beyond K/32 = 256) the MFMA small-batch
+    decode with 2 / 4 token columns and 4 (K/32 <= 256) or 8 stages per lane, M >= 5 the MFMA prefill kernels;
+    the sumi hook names the same instantiation."""
+    import quant_gemm as qg
+    cases = [((1, 4096, 4096), "gemvt F=2 MT=1 "), ((2, 4096, 4096), "gemvt F=2 MT=2 "),
+             ((2, 4096, 8192), "gemvt F=2 MT=2 "), ((2, 4096, 8224), "gemvm F=2 NU=8 MP=2 "),
+             ((2, 4096, 14336), "gemvm F=2 NU=8 MP=2 W=14 "), ((3, 4096, 4096), "gemvm F=2 NU=4 MP=4 W=8 "),
+             ((4, 4096, 14336), "gemvm F=2 NU=8 MP=4 W=14 "), ((4, 64, 160), "gemvm F=2 NU=4 MP=4 W=1 "),
+             ((5, 4096, 14336), "mmq F=2 "), ((8, 4096, 4096), "mmq F=2 ")]
+    for (m, n, k), fam in cases:
+        cfg = qg.debug_config_tiled(m, n, k, 2)
+        assert cfg.startswith(fam), (m, n, k, cfg)
+        assert cfg == qg.debug_config_tiled(m, n, k, 2, sumi=True)
+        if fam.startswith("gem"):  # the tiled-activation entry: the same kernel, activations from the tiled layout
+            cfg_ta = qg.debug_config_tiled_act(m, n, k, 2)
+            assert cfg_ta.startswith(fam) and " TA=1 " in cfg_ta, cfg_ta
+    # every format takes the small-batch decode; K beyond 16 waves (K > 16384) goes to the MFMA prefill kernel
+    for t in (3, 6, 7, 8):
+        assert qg.debug_config_tiled(4, 4096, 14336, t).startswith(f"gemvm F={t} NU=8 MP=4 ")
+    assert qg.debug_config_tiled(4, 4096, 16416, 2).startswith("mmq ")
+
+
 def test_ldc_entry_validates(lib):
     so = lib.load()
     P = ctypes.c_void_p
