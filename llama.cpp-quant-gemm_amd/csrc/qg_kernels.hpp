@@ -86,7 +86,8 @@ hipError_t launch_gemv(const GemmArgs& g, hipStream_t st);
 
 // The decode GEMV (M <= 4) on the tiled layout (qg_gemvt.hip, round 6): waves of 16 rows x 4 stages reading
 // whole 256-B plane runs, the row kernel's dot and per-block terms (bit-identical per block to the
-// reference's), fixed summation order.
+// reference's), fixed summation order. run_tiled sends it M = 1..2 up to K/32 = 256; M = 3..4 only in builds
+// without the small-batch decode (QG_TILED_GEMVM=0, A/B).
 bool gemvt_eligible(const GemmArgs& g);
 hipError_t launch_gemvt(const GemmArgs& g, hipStream_t st);
 
